@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mvoxel-smooths/s at 512^3 fp32 (BASELINE.json metric),
+plus V-cycles/s, HBM roofline fraction of the smoother kernel and the CPU
+baseline (the fp64 oracle, 1 thread, bounded sample).
+
+Workload (config C4 of BASELINE.json, the largest single-GPU config the metric
+is quoted on): 512^3 fp32 image, VED-form full 3x3 diffusion tensor (synthetic,
+generated on the device), dt 0.1, unit spacing, 4-colour Gauss-Seidel smoother.
+One step = one level-0 smoother sweep (all colours) over the whole volume.
+
+    python bench.py [--gpus N --steps K --warmup W]
+For N > 1 the driver launches one process per GPU (torch.distributed.run);
+the volume is split into z-slabs (strong scaling, fixed 512^3) with RCCL halo
+exchanges.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+BYTES_PER_VOXEL_SMOOTH = 36.0   # u in 4 + b 4 + u out 4 + 6-comp tensor 24
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--vcycles", type=int, default=5)
+    p.add_argument("--smoother", default="gs", choices=["gs", "wj"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    return p.parse_args()
+
+
+def cpu_baseline(seconds):
+    """fp64 oracle (restated reference algorithm, lexicographic GS, 1 thread) on a
+    bounded 128^3 sample of the same VED-form workload."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    import synth
+    shape = (128, 128, 128)
+    T = synth.ved_form(shape)
+    o = oracle.Oracle(shape, (1.0, 1.0, 1.0), T, 0.1)
+    b = synth.image(shape, seed=3)
+    x = b.copy()
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        x = o.gs_lex(0, x, b)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    nvox = float(np.prod(shape))
+    return {"value": nvox * n / el / 1e6, "unit": "Mvoxel-smooths/s", "cores": 1, "kind": "port",
+            "sample": f"128^3 VED-form full tensor, {n} lexicographic GS sweeps, fp64, "
+                      f"oracle/ (line-faithful restatement of the ITK reference), {el:.1f} s"}
+
+
+def load_traffic(tag):
+    path = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(a.gpus, world)
+    dist = None
+    if world > 1:
+        import torch  # noqa: F401  (torch first: our library then binds to the same HIP runtime)
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    import multigridanisotropicdiffusion_amd as M
+
+    S = a.size
+    gshape = (S, S, S)
+    nz_local = S // world
+    shape = (nz_local, S, S)
+    sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
+    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
+                 nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape)
+    if world > 1:
+        import torch
+        uid = M.comm_unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, src=0)
+        s.comm_init(bytes(t.tolist()))
+    s.synth_tensor(kind=0, seed=4)
+    s.setup()
+    s.synth_level(0, M.capi.B, 3)
+    s.synth_level(0, M.capi.X, 3)
+    s.synchronize()
+
+    def barrier():
+        s.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    # warmup
+    if a.warmup:
+        s.bench_smooth(0, a.warmup)
+    barrier()
+    t0 = time.perf_counter()
+    dev_ms, kern_ms, launches = s.bench_smooth(0, a.steps)
+    barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt[0])
+    nvox = float(S) ** 3
+    value = nvox * a.steps / wall / 1e6
+    # V-cycles/s (same volume, nu = 2)
+    s.vcycle()
+    barrier()
+    t1 = time.perf_counter()
+    vc_ms = s.bench_vcycle(a.vcycles)
+    barrier()
+    vwall = time.perf_counter() - t1
+    if dist is not None:
+        import torch
+        tt = torch.tensor([vwall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        vwall = float(tt[0])
+    info = s.level_info(0)
+    nlev = s.num_levels
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+    # roofline of the dominant kernel: per launch one colour class = 1/ncolors of the slab
+    ncolors = 4 if a.smoother == "gs" else 1
+    units_per_launch = float(shape[0] * shape[1] * shape[2]) / ncolors
+    achieved = BYTES_PER_VOXEL_SMOOTH * units_per_launch / (kern_ms * 1e-3) / 1e9
+    tag = f"{a.smoother}_{S}"
+    traffic = load_traffic(tag)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4),
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "kernel": "gs_color_k<float,3,FULL>" if a.smoother == "gs" else "wj_k<float,3,FULL>",
+            "kernel_ms_mean": round(kern_ms, 5), "launches": launches,
+            "algorithmic_bytes_per_launch": BYTES_PER_VOXEL_SMOOTH * units_per_launch}
+    if traffic:
+        roof["traffic_source"] = traffic.get("source")
+    line = {
+        "metric": "Mvoxel-smooths/s (and V-cycles/s) at 512^3 fp32; achieved HBM GB/s vs peak",
+        "value": round(value, 1),
+        "unit": "Mvoxel-smooths/s",
+        "n_gpus": n_gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(wall / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (device-generated VED-form tensor and counter-hash image)",
+        "config": {"workload": f"C4 {S}^3 VED-form full tensor, "
+                               f"{'4-colour Gauss-Seidel' if a.smoother == 'gs' else 'weighted Jacobi'}"
+                               f" level-0 sweeps", "global_shape": list(gshape),
+                   "levels": nlev, "time_step": 0.1, "parallelism": f"z-slab x{world}",
+                   "slab_shape": list(info["shape"])},
+        "vcycles_per_s": round(a.vcycles / vwall, 3),
+        "ms_per_vcycle": round(vwall / a.vcycles * 1e3, 3),
+        "device_ms_per_step": round(dev_ms / a.steps, 4),
+        "roofline": roof,
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        cb = cpu_baseline(a.cpu_seconds)
+        line["cpu_baseline"] = cb
+    else:
+        line["cpu_baseline"] = None
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,220 @@
+/*
+ * mad.h -- C ABI of the MI355X-native multigrid anisotropic-diffusion solver.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (nellogrb/MultigridAnisotropicDiffusion, ITK remote module).  Plain C types
+ * only: sizes, pointers, enums.  Every entry point names the reference
+ * interface it replaces (paths relative to the reference repository root):
+ *
+ *   MAD = include/itkMultigridAnisotropicDiffusionImageFilter.{h,hxx}
+ *   SM  = include/mad/itkMultigridSmoother.h (smoother plug-in interface)
+ *   IGO = include/mad/itkInterGridOperators.{h,hxx}
+ *   GH  = include/mad/itkGridsHierarchy.{h,hxx}
+ *   DS  = include/mad/itkDirectSolver.{h,hxx}
+ *
+ * Conventions
+ *   - status: every call returns MAD_OK (0) or a mad_status error code; the
+ *     message is available from mad_last_error(ctx) (or mad_last_error(NULL)
+ *     for errors raised before a context exists).  The reference raises no
+ *     errors (it has no validation); the checks here are additions.
+ *   - images are x-fastest (ITK buffer order), size[] / spacing[] x first.
+ *   - a context owns all device memory and one HIP stream; it is not
+ *     re-entrant (same as the reference filter, MAD.h:185 m_CurrentLevel).
+ */
+#ifndef MAD_H
+#define MAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAD_ABI_VERSION 1
+
+typedef enum mad_status {
+  MAD_OK = 0,
+  MAD_ERR_INVALID = 1,     /* bad argument (size, dim, dtype, level, region mismatch) */
+  MAD_ERR_STATE = 2,       /* call out of order (e.g. run before set_tensor) */
+  MAD_ERR_DEVICE = 3,      /* HIP runtime error */
+  MAD_ERR_COMM = 4,        /* RCCL / multi-GPU error */
+  MAD_ERR_SINGULAR = 5,    /* coarsest operator singular */
+  MAD_ERR_UNSUPPORTED = 6, /* valid request this build does not implement */
+  MAD_ERR_NOMEM = 7,
+  MAD_ERR_NUMERIC = 8      /* NaN/Inf residual */
+} mad_status;
+
+/* MAD.h:123 enum CycleType { VCYCLE, FMG, SMOOTHER } -- same values */
+typedef enum mad_cycle { MAD_VCYCLE = 0, MAD_FMG = 1, MAD_SMOOTHER = 2 } mad_cycle;
+
+/* smoother plug-in (template argument TSmootherType, MAD.h:89-92) */
+typedef enum mad_smoother {
+  MAD_GAUSS_SEIDEL = 0,      /* multicolour GS: red-black for 5/7-point operators (isotropic or
+                                diagonal tensor), 4 colours for 9/19-point (full tensor).
+                                Replaces mad::MultigridGaussSeidelSmoother (parity at convergence). */
+  MAD_GAUSS_SEIDEL_LEX = 1,  /* exact lexicographic GS order via hyperplane wavefronts
+                                (per-sweep parity with the reference; slow, debug/parity mode) */
+  MAD_WEIGHTED_JACOBI = 2    /* mad::MultigridWeightedJacobiSmoother (ω = 2/3 default) */
+} mad_smoother;
+
+typedef enum mad_dtype {
+  MAD_U8 = 0, MAD_I8 = 1, MAD_U16 = 2, MAD_I16 = 3, MAD_U32 = 4, MAD_I32 = 5,
+  MAD_F32 = 6, MAD_F64 = 7
+} mad_dtype;
+
+typedef enum mad_precision { MAD_FP32 = 0, MAD_FP64 = 1 } mad_precision;
+
+typedef enum mad_tensor_kind {
+  MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */
+  MAD_TENSOR_ISOTROPIC = 1,  /* M = c(x) I */
+  MAD_TENSOR_DIAGONAL = 2,   /* off-diagonals identically 0 */
+  MAD_TENSOR_FULL = 3
+} mad_tensor_kind;
+
+/* per-level device arrays addressable through the kernel-level entry points */
+typedef enum mad_which { MAD_X = 0 /* solution */, MAD_B = 1 /* rhs */, MAD_R = 2 /* residual */ } mad_which;
+
+/* Filter parameters: the MultigridAnisotropicDiffusionImageFilter setters
+ * (MAD.h:133-160) plus the image geometry and MI355X execution options.
+ * mad_desc_init() fills the reference defaults (MAD.hxx:36-52). */
+typedef struct mad_desc {
+  uint32_t abi_version;          /* = MAD_ABI_VERSION */
+  int32_t dim;                   /* TInputImage::ImageDimension: 2 or 3 */
+  int64_t size[3];               /* image size, x first; size[2] = 1 in 2D */
+  double spacing[3];             /* image spacing, x first (tensor spacing is ignored, as in GH:131) */
+  int32_t cycle;                 /* SetCycle,              default MAD_VCYCLE */
+  int32_t smoother;              /* TSmootherType,         default MAD_GAUSS_SEIDEL */
+  uint32_t iterations_per_grid;  /* SetIterationsPerGrid,  default 2 */
+  uint32_t max_cycles;           /* SetMaxCycles,          default 100 */
+  uint32_t number_of_steps;      /* SetNumberOfSteps,      default 1 */
+  double time_step;              /* SetTimeStep,           default 0.01 */
+  double tolerance;              /* SetTolerance,          default 1e-6 */
+  double omega;                  /* WJ weight (MultigridWeightedJacobiSmoother ctor), default 2/3 */
+  int32_t verbose;               /* SetVerbose,            default 0 */
+  int32_t precision;             /* MAD_FP32 (default) or MAD_FP64 storage + arithmetic */
+  int32_t stall_guard;           /* 1: end a time step once relres stops improving (the fp32
+                                    floor); default 1 for FP32, 0 for FP64 */
+  int32_t device;                /* HIP device ordinal, -1 = current device */
+  int32_t tensor_kind;           /* mad_tensor_kind, default AUTO */
+  int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
+  int32_t rank;                  /* this rank */
+  int32_t reserved[9];
+} mad_desc;
+
+typedef struct mad_stats {
+  uint32_t steps;                /* time steps run */
+  uint32_t total_cycles;         /* V-cycles / FMG cycles / smoother iterations over all steps */
+  uint32_t last_cycles;          /* cycles of the last time step */
+  int32_t stalled;               /* 1 if the stall guard ended any step before tolerance */
+  double last_relres;            /* relative residual ||b - A x|| / ||b|| at the end */
+  double setup_ms;               /* hierarchy + operators + coarse LU */
+  double solve_ms;               /* time-step loop (device time, host-synchronised) */
+  uint32_t num_levels;
+  int32_t tensor_kind;           /* resolved mad_tensor_kind */
+  int32_t colors;                /* GS colours used (2 or 4) */
+  int32_t reserved[5];
+} mad_stats;
+
+typedef struct mad_ctx mad_ctx;
+
+/* ---------------------------------------------------------------- setup */
+int mad_desc_init(mad_desc *d);                       /* MAD.hxx:36-52 defaults */
+int mad_max_depth(int32_t dim, const int64_t size[3]);/* GH.hxx:36-59 depth rule (-1 on error) */
+int mad_create(const mad_desc *d, mad_ctx **out);     /* MAD::New() + setters */
+void mad_destroy(mad_ctx *ctx);
+const char *mad_last_error(const mad_ctx *ctx);
+int mad_get_desc(const mad_ctx *ctx, mad_desc *out);
+
+/* SetDiffusionTensor (MAD.hxx:66-101): AoS symmetric tensors, ITK
+ * SymmetricSecondRankTensor component order [xx,xy,xz,yy,yz,zz] (3D) /
+ * [xx,xy,yy] (2D), dtype MAD_F32 or MAD_F64.  Copied (cast to fp64) at call time. */
+int mad_set_tensor(mad_ctx *ctx, const void *host_aos, int32_t dtype);
+int mad_set_tensor_device(mad_ctx *ctx, const void *dev_aos, int32_t dtype);
+
+/* Build the grids hierarchy, per-level operators and the coarsest-grid direct
+ * solver (GH.hxx:30-204, DS.hxx:32-88).  Implicit in mad_run; explicit for the
+ * kernel-level entry points below. */
+int mad_setup(mad_ctx *ctx);
+
+/* ---------------------------------------------------------------- filter */
+/* GenerateData (MAD.hxx:104-297): cast input -> internal precision, run
+ * NumberOfSteps implicit-Euler steps, each solved by the chosen cycle to
+ * Tolerance / MaxCycles, cast to the output type (static_cast semantics:
+ * truncation toward zero for integer outputs, saturated to the type's range). */
+int mad_run(mad_ctx *ctx, const void *host_in, int32_t in_dtype, void *host_out,
+            int32_t out_dtype, mad_stats *stats);
+/* same with device-resident input/output buffers (no PCIe in the solve) */
+int mad_run_device(mad_ctx *ctx, const void *dev_in, int32_t in_dtype, void *dev_out,
+                   int32_t out_dtype, mad_stats *stats);
+/* per-time-step history of the last run */
+int mad_get_step_stats(const mad_ctx *ctx, uint32_t step, uint32_t *cycles, double *relres);
+
+/* ---------------------------------------------------------------- hierarchy */
+int mad_num_levels(const mad_ctx *ctx);               /* GH::GetMaxDepth() + 1 */
+/* Host-only plan of the hierarchy for a descriptor (no device needed): returns
+ * the number of levels (or -status on error) and fills level `level`'s global
+ * size, spacing, centring and this rank's z-slab [z_begin, z_end); replicated
+ * (agglomerated) levels report the full range with distributed = 0.
+ * GH.hxx:36-106 plus the MI355X z-slab rule. */
+int mad_plan_level(const mad_desc *d, int32_t level, int64_t size[3], double spacing[3],
+                   int32_t centering[3], int64_t *z_begin, int64_t *z_end,
+                   int32_t *distributed);
+/* GetRegionAtLevel / GetSpacingAtLevel / GetVertexCenteringAtLevel (GH.h:96-106):
+ * centering 0 = vertex, 1 = cell (level 0 reports vertex, GH.hxx:207).
+ * size is this rank's slab on multi-GPU runs. */
+int mad_level_info(const mad_ctx *ctx, int32_t level, int64_t size[3], double spacing[3],
+                   int32_t centering[3]);
+
+/* ---------------------------------------------------------------- kernel level */
+/* Host <-> device copies of one level array (fp64 on the host, converted). */
+int mad_upload(mad_ctx *ctx, int32_t level, int32_t which, const double *host);
+int mad_download(mad_ctx *ctx, int32_t level, int32_t which, double *host);
+int mad_fill(mad_ctx *ctx, int32_t level, int32_t which, double value);
+/* SM.h:60-62 SingleIteration, applied `sweeps` times in place: x <- S(x, b). */
+int mad_smooth(mad_ctx *ctx, int32_t level, uint32_t sweeps);
+/* SM.h:66-68 ComputeResidual: r <- b - A x; optional ||r||_2 (MAD.hxx:496-515). */
+int mad_residual(mad_ctx *ctx, int32_t level, double *norm_out);
+/* MAD.hxx:496-515 L2Norm of one level array (fp64 accumulation). */
+int mad_norm(mad_ctx *ctx, int32_t level, int32_t which, double *norm_out);
+/* IGO.hxx:175-304 Restriction: b[level+1] <- R r[level]. */
+int mad_restrict(mad_ctx *ctx, int32_t level);
+/* IGO.hxx:45-172 Interpolation: x[level] <- P x[level+1]. */
+int mad_interpolate(mad_ctx *ctx, int32_t level);
+/* IGO Interpolation + correction add (MAD.hxx:422-435): x[level] += P x[level+1]. */
+int mad_prolongate_add(mad_ctx *ctx, int32_t level);
+/* DS.hxx:91-147 DirectSolver::Solve on the coarsest level: x[L] <- A_L^-1 b[L]. */
+int mad_coarse_solve(mad_ctx *ctx);
+/* MAD.hxx:341-493 VCycle on level 0 (x[0], b[0]) -- one cycle. */
+int mad_vcycle(mad_ctx *ctx);
+/* MAD.hxx:300-338 FullMultiGrid: x[0] <- FMG(b[0]). */
+int mad_fmg(mad_ctx *ctx);
+int mad_synchronize(mad_ctx *ctx);
+
+/* ---------------------------------------------------------------- measurement */
+/* Time `sweeps` smoother sweeps on `level` with HIP events on the context
+ * stream: total wall (device) time, and the mean duration of the dominant
+ * (sweep) kernel launches.  Used by bench.py. */
+int mad_bench_smooth(mad_ctx *ctx, int32_t level, uint32_t sweeps, double *total_ms,
+                     double *kernel_ms_mean, uint32_t *kernel_launches);
+/* Time `cycles` V-cycles (device time). */
+int mad_bench_vcycle(mad_ctx *ctx, uint32_t cycles, double *total_ms);
+/* Deterministic synthetic inputs generated on the device (bench / smoke):
+ * kind 0 = VED-form tensor, 1 = isotropic c(x)I, 2 = random-rotation SPD.
+ * Counter-based, identical to tests/synth.py's *_dev formulas. */
+int mad_bench_synth_tensor(mad_ctx *ctx, int32_t kind, uint64_t seed);
+int mad_bench_synth_level(mad_ctx *ctx, int32_t level, int32_t which, uint64_t seed);
+
+/* ---------------------------------------------------------------- multi-GPU */
+/* z-slab decomposition over `nranks` processes, one GPU each, RCCL halos.
+ * The unique id (128 bytes) is created on rank 0 and broadcast by the host. */
+int mad_comm_unique_id(void *uid128);
+int mad_comm_init(mad_ctx *ctx, const void *uid128);
+/* slab [z_begin, z_end) of this rank for a global nz (even-aligned split) */
+int mad_slab_range(int64_t nz, int32_t nranks, int32_t rank, int32_t align, int64_t *z_begin,
+                   int64_t *z_end);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAD_H */

@@ -1,0 +1,167 @@
+"""ctypes binding of include/mad.h (the C ABI of libmad_hip.so).
+
+The shared library is built in-tree (``python -m multigridanisotropicdiffusion_amd.build``
+or ``__graft_entry__.build()``).  There is no fallback: if the library is
+missing, importing this module raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmad_hip.so")
+
+ABI_VERSION = 1
+
+# mad_status
+OK, ERR_INVALID, ERR_STATE, ERR_DEVICE, ERR_COMM, ERR_SINGULAR, ERR_UNSUPPORTED, ERR_NOMEM, \
+    ERR_NUMERIC = range(9)
+# mad_cycle (itkMultigridAnisotropicDiffusionImageFilter.h:123)
+VCYCLE, FMG, SMOOTHER = 0, 1, 2
+# mad_smoother
+GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, WEIGHTED_JACOBI = 0, 1, 2
+# mad_dtype
+U8, I8, U16, I16, U32, I32, F32, F64 = range(8)
+# mad_precision
+FP32, FP64 = 0, 1
+# mad_tensor_kind
+TENSOR_AUTO, TENSOR_ISOTROPIC, TENSOR_DIAGONAL, TENSOR_FULL = range(4)
+# mad_which
+X, B, R = 0, 1, 2
+
+EXPORTS = (
+    "mad_desc_init", "mad_max_depth", "mad_create", "mad_destroy", "mad_last_error",
+    "mad_get_desc", "mad_set_tensor", "mad_set_tensor_device", "mad_setup", "mad_run",
+    "mad_run_device", "mad_get_step_stats", "mad_num_levels", "mad_plan_level",
+    "mad_level_info", "mad_upload",
+    "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
+    "mad_interpolate", "mad_prolongate_add", "mad_coarse_solve", "mad_vcycle", "mad_fmg",
+    "mad_synchronize", "mad_bench_smooth", "mad_bench_vcycle", "mad_bench_synth_tensor",
+    "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_slab_range",
+)
+
+
+class MadDesc(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_uint32),
+        ("dim", ctypes.c_int32),
+        ("size", ctypes.c_int64 * 3),
+        ("spacing", ctypes.c_double * 3),
+        ("cycle", ctypes.c_int32),
+        ("smoother", ctypes.c_int32),
+        ("iterations_per_grid", ctypes.c_uint32),
+        ("max_cycles", ctypes.c_uint32),
+        ("number_of_steps", ctypes.c_uint32),
+        ("time_step", ctypes.c_double),
+        ("tolerance", ctypes.c_double),
+        ("omega", ctypes.c_double),
+        ("verbose", ctypes.c_int32),
+        ("precision", ctypes.c_int32),
+        ("stall_guard", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("tensor_kind", ctypes.c_int32),
+        ("nranks", ctypes.c_int32),
+        ("rank", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 9),
+    ]
+
+
+class MadStats(ctypes.Structure):
+    _fields_ = [
+        ("steps", ctypes.c_uint32),
+        ("total_cycles", ctypes.c_uint32),
+        ("last_cycles", ctypes.c_uint32),
+        ("stalled", ctypes.c_int32),
+        ("last_relres", ctypes.c_double),
+        ("setup_ms", ctypes.c_double),
+        ("solve_ms", ctypes.c_double),
+        ("num_levels", ctypes.c_uint32),
+        ("tensor_kind", ctypes.c_int32),
+        ("colors", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+class MadError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mad error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load libmad_hip.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build the HIP library first "
+            "(python -m multigridanisotropicdiffusion_amd.build)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, u32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64, \
+        ctypes.c_double
+    dp = ctypes.POINTER(ctypes.c_double)
+    i64p = ctypes.POINTER(ctypes.c_int64)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    sig = {
+        "mad_desc_init": ([ctypes.POINTER(MadDesc)], i32),
+        "mad_max_depth": ([i32, i64p], i32),
+        "mad_create": ([ctypes.POINTER(MadDesc), ctypes.POINTER(vp)], i32),
+        "mad_destroy": ([vp], None),
+        "mad_last_error": ([vp], ctypes.c_char_p),
+        "mad_get_desc": ([vp, ctypes.POINTER(MadDesc)], i32),
+        "mad_set_tensor": ([vp, vp, i32], i32),
+        "mad_set_tensor_device": ([vp, vp, i32], i32),
+        "mad_setup": ([vp], i32),
+        "mad_run": ([vp, vp, i32, vp, i32, ctypes.POINTER(MadStats)], i32),
+        "mad_run_device": ([vp, vp, i32, vp, i32, ctypes.POINTER(MadStats)], i32),
+        "mad_get_step_stats": ([vp, u32, u32p, dp], i32),
+        "mad_num_levels": ([vp], i32),
+        "mad_plan_level": ([ctypes.POINTER(MadDesc), i32, i64p, dp, i32p, i64p, i64p, i32p], i32),
+        "mad_level_info": ([vp, i32, i64p, dp, i32p], i32),
+        "mad_upload": ([vp, i32, i32, dp], i32),
+        "mad_download": ([vp, i32, i32, dp], i32),
+        "mad_fill": ([vp, i32, i32, dbl], i32),
+        "mad_smooth": ([vp, i32, u32], i32),
+        "mad_residual": ([vp, i32, dp], i32),
+        "mad_norm": ([vp, i32, i32, dp], i32),
+        "mad_restrict": ([vp, i32], i32),
+        "mad_interpolate": ([vp, i32], i32),
+        "mad_prolongate_add": ([vp, i32], i32),
+        "mad_coarse_solve": ([vp], i32),
+        "mad_vcycle": ([vp], i32),
+        "mad_fmg": ([vp], i32),
+        "mad_synchronize": ([vp], i32),
+        "mad_bench_smooth": ([vp, i32, u32, dp, dp, u32p], i32),
+        "mad_bench_vcycle": ([vp, u32, dp], i32),
+        "mad_bench_synth_tensor": ([vp, i32, ctypes.c_uint64], i32),
+        "mad_bench_synth_level": ([vp, i32, i32, ctypes.c_uint64], i32),
+        "mad_comm_unique_id": ([vp], i32),
+        "mad_comm_init": ([vp, vp], i32),
+        "mad_slab_range": ([i64, i32, i32, i32, i64p, i64p], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc, ctx=None):
+    if rc != OK:
+        msg = load().mad_last_error(ctx)
+        raise MadError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def default_desc():
+    d = MadDesc()
+    check(load().mad_desc_init(ctypes.byref(d)))
+    return d

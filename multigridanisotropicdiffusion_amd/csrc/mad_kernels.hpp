@@ -1,0 +1,610 @@
+// mad_kernels.hpp -- HIP kernels for the V-cycle hot path (gfx950 / CDNA4).
+//
+// Operator: the reference assembles a 27-coefficient DCA stencil per voxel
+// (include/mad/itkGridsHierarchy.hxx:298-516).  Here it is evaluated
+// matrix-free from per-level coefficient fields (SoA, storage type T):
+//
+//   a_d   = dt M_dd / h_d^2                 (ISO: one field a, a_d = a * rat[d])
+//   g_d   = dt/(2h_d) sum_d2 delta_d2 M_d,d2 / (2h_d2)   (one-sided at the border)
+//   e_dd2 = dt M_dd2 / (2 h_d h_d2)         (FULL only)
+//   (A u)(p) = D u(p) - S(p),   D = 1 + 2 sum a_d
+//   S(p) = sum_d (a_d+g_d) u~(p+e_d) + (a_d-g_d) u~(p-e_d)
+//        + sum_{d<d2} e_dd2 (u~(++) - u~(+-) - u~(-+) + u~(--))
+//   u~ mirrored about the boundary node: u~(-1) = u(1), u~(n) = u(n-2)
+//
+// which equals the DCA stencil row by row (tests/test_oracle.py checks it to
+// 1e-13).  Coefficient field order: [a.. | g.. | e..] (see CoefLayout).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mad {
+
+enum { KISO = 1, KDIAG = 2, KFULL = 3 };
+
+template <int DIM, int KIND>
+struct CoefLayout {
+  static constexpr int NA = (KIND == KISO) ? 1 : DIM;
+  static constexpr int NG = DIM;
+  static constexpr int NE = (KIND == KFULL) ? DIM * (DIM - 1) / 2 : 0;
+  static constexpr int N = NA + NG + NE;
+};
+
+inline int coef_count(int dim, int kind) {
+  int na = (kind == KISO) ? 1 : dim;
+  int ne = (kind == KFULL) ? dim * (dim - 1) / 2 : 0;
+  return na + dim + ne;
+}
+
+// Geometry of one level slab as seen by a kernel.  Arrays are x-fastest; the
+// base pointer addresses local plane 0; in 3D one ghost plane is allocated on
+// each side (used for rank halos; at a global boundary the mirror is used).
+struct Geo {
+  int nx, ny, nz;       // local sizes
+  int zoff;             // global z index of local plane 0 (colour parity)
+  int zlo_ghost;        // 1: plane -1 holds the lower neighbour's data
+  int zhi_ghost;        // 1: plane nz holds the upper neighbour's data
+  int64_t sy, sz;       // strides
+  int64_t N;            // nx*ny*nz (coefficient field stride)
+};
+
+template <typename T>
+struct Rat {
+  T r[3];  // ISO spacing ratios h_x^2 / h_d^2
+};
+
+// ---------------------------------------------------------------------------
+// the per-point stencil: D and S of (A u)(p) = D u(p) - S(p)
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* __restrict__ cf,
+                                              const Geo& g, const Rat<T>& rat, int i, int j,
+                                              int k, int64_t p, T& D, T& S) {
+  using L = CoefLayout<DIM, KIND>;
+  const int64_t N = g.N;
+  const int64_t dxm = (i == 0) ? 1 : -1;
+  const int64_t dxp = (i == g.nx - 1) ? -1 : 1;
+  const int64_t dym = (j == 0) ? g.sy : -g.sy;
+  const int64_t dyp = (j == g.ny - 1) ? -g.sy : g.sy;
+  T ax, ay, az = T(0);
+  if (KIND == KISO) {
+    const T a = cf[p];
+    ax = a;
+    ay = a * rat.r[1];
+    if (DIM == 3) az = a * rat.r[2];
+  } else {
+    ax = cf[p];
+    ay = cf[N + p];
+    if (DIM == 3) az = cf[2 * N + p];
+  }
+  const T gx = cf[L::NA * N + p];
+  const T gy = cf[(L::NA + 1) * N + p];
+  T s = (ax + gx) * u[p + dxp] + (ax - gx) * u[p + dxm] + (ay + gy) * u[p + dyp] +
+        (ay - gy) * u[p + dym];
+  T d = T(1) + T(2) * (ax + ay);
+  int64_t dzm = 0, dzp = 0;
+  if (DIM == 3) {
+    dzm = (k == 0 && !g.zlo_ghost) ? g.sz : -g.sz;
+    dzp = (k == g.nz - 1 && !g.zhi_ghost) ? -g.sz : g.sz;
+    const T gz = cf[(L::NA + 2) * N + p];
+    s += (az + gz) * u[p + dzp] + (az - gz) * u[p + dzm];
+    d += T(2) * az;
+  }
+  if (KIND == KFULL) {
+    constexpr int E0 = L::NA + L::NG;
+    const T exy = cf[E0 * N + p];
+    s += exy * (u[p + dxp + dyp] - u[p + dxp + dym] - u[p + dxm + dyp] + u[p + dxm + dym]);
+    if (DIM == 3) {
+      const T exz = cf[(E0 + 1) * N + p];
+      const T eyz = cf[(E0 + 2) * N + p];
+      s += exz * (u[p + dxp + dzp] - u[p + dxp + dzm] - u[p + dxm + dzp] + u[p + dxm + dzm]);
+      s += eyz * (u[p + dyp + dzp] - u[p + dyp + dzm] - u[p + dym + dzp] + u[p + dym + dzm]);
+    }
+  }
+  D = d;
+  S = s;
+}
+
+// ---------------------------------------------------------------------------
+// multicolour Gauss-Seidel, one colour per launch, in place.
+//   ncolors 2: red-black, colour = (i+j+k) & 1        (5/7-point operators)
+//   ncolors 4: 3D colour = ((i+k)&1) | ((j+k)&1)<<1   (19-point; corners inactive)
+//              2D colour = (i&1) | (j&1)<<1           (9-point)
+// Same-colour points are never neighbours, so a colour pass is order-free.
+// Thread (x, y, z) -> i' (half row), row index, plane.
+template <typename T, int DIM, int KIND>
+__global__ void __launch_bounds__(256) gs_color_k(T* __restrict__ u, const T* __restrict__ b,
+                                                  const T* __restrict__ cf, Geo g, Rat<T> rat,
+                                                  int color, int ncolors) {
+  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int kg = k + g.zoff;
+  const int jq = blockIdx.y * blockDim.y + threadIdx.y;
+  const int iq = blockIdx.x * blockDim.x + threadIdx.x;
+  int i, j;
+  if (ncolors == 4) {
+    if (DIM == 3) {
+      j = 2 * jq + (((color >> 1) ^ kg) & 1);
+      i = 2 * iq + (((color & 1) ^ kg) & 1);
+    } else {
+      j = 2 * jq + (color >> 1);
+      i = 2 * iq + (color & 1);
+    }
+  } else {
+    j = jq;
+    i = 2 * iq + ((color + j + kg) & 1);
+  }
+  if (i >= g.nx || j >= g.ny) return;
+  const int64_t p = i + g.sy * j + g.sz * k;
+  T D, S;
+  stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
+  u[p] = (b[p] + S) / D;
+}
+
+// exact lexicographic GS (reference order, itkMultigridGaussSeidelSmoother.hxx:67-106)
+// as hyperplane wavefronts t = i + 2j + 3k (3D) / i + 2j (2D): every lex-earlier
+// neighbour lies on an earlier hyperplane, every later one on a later hyperplane.
+template <typename T, int DIM, int KIND>
+__global__ void __launch_bounds__(256) gs_lex_plane_k(T* __restrict__ u, const T* __restrict__ b,
+                                                      const T* __restrict__ cf, Geo g, Rat<T> rat,
+                                                      int t) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = (DIM == 3) ? (int)blockIdx.y : 0;
+  if (j >= g.ny) return;
+  const int i = t - 2 * j - 3 * k;
+  if (i < 0 || i >= g.nx) return;
+  const int64_t p = i + g.sy * j + g.sz * k;
+  T D, S;
+  stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
+  u[p] = (b[p] + S) / D;
+}
+
+// ---------------------------------------------------------------------------
+// fp64 block reduction helper (wave64 shuffles, then LDS across waves)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+template <int NT>
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double red[NT / 64];
+  const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+  v = wave_sum(v);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (tid == 0) {
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) s += red[w];
+  }
+  return s;  // valid in thread 0
+}
+
+// weighted Jacobi sweep (itkMultigridWeightedJacobiSmoother.hxx:67-98), out of place
+template <typename T, int DIM, int KIND>
+__global__ void __launch_bounds__(256) wj_k(const T* __restrict__ u, T* __restrict__ uo,
+                                            const T* __restrict__ b, const T* __restrict__ cf,
+                                            Geo g, Rat<T> rat, T omega) {
+  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.nx || j >= g.ny) return;
+  const int64_t p = i + g.sy * j + g.sz * k;
+  T D, S;
+  stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
+  T v = (b[p] + S) * (omega / D);
+  v += (T(1) - omega) * u[p];
+  uo[p] = v;
+}
+
+// residual r = b - A u (itkMultigridGaussSeidelSmoother.hxx:148-176), with optional
+// fp64 ||r||^2 block partials (L2Norm, MAD.hxx:496-515)
+template <typename T, int DIM, int KIND>
+__global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const T* __restrict__ b,
+                                                  T* __restrict__ r, const T* __restrict__ cf,
+                                                  Geo g, Rat<T> rat, double* __restrict__ part) {
+  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  double sq = 0.0;
+  if (i < g.nx && j < g.ny) {
+    const int64_t p = i + g.sy * j + g.sz * k;
+    T D, S;
+    stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
+    const T rv = b[p] - (D * u[p] - S);
+    r[p] = rv;
+    sq = (double)rv * (double)rv;
+  }
+  if (part) {
+    const double s = block_sum<256>(sq);
+    if (threadIdx.x == 0 && threadIdx.y == 0)
+      part[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = s;
+  }
+}
+
+// sum of squares of a contiguous array, grid-stride, fp64 partials per block
+template <typename T>
+__global__ void __launch_bounds__(256) sumsq_k(const T* __restrict__ x, int64_t n,
+                                               double* __restrict__ part) {
+  double s = 0.0;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const double v = (double)x[q];
+    s += v * v;
+  }
+  s = block_sum<256>(s);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// deterministic final reduction of partials (one block)
+__global__ void __launch_bounds__(256) reduce_final_k(const double* __restrict__ part, int64_t n,
+                                                      double* __restrict__ out) {
+  double s = 0.0;
+  for (int64_t q = threadIdx.x; q < n; q += blockDim.x) s += part[q];
+  s = block_sum<256>(s);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// ---------------------------------------------------------------------------
+// inter-grid transfers (itkInterGridOperators.{h,hxx}), gather form, separable.
+// Restriction taps for coarse index I (IGO.h:115-127): vertex interior 1/4,1/2,1/4
+// about 2I, injection at the two ends; cell interior 1/8,3/8,3/8,1/8 on 2I-1..2I+2,
+// left 1/2,3/8,1/8 on 0..2, right 1/8,3/8,1/2 on 2I-1..2I+1.
+__device__ __forceinline__ int restrict_taps(int I, int nc, int cell, int* idx, double* w) {
+  if (!cell) {
+    if (I == 0 || I == nc - 1) {
+      idx[0] = 2 * I; w[0] = 1.0;
+      return 1;
+    }
+    idx[0] = 2 * I - 1; idx[1] = 2 * I; idx[2] = 2 * I + 1;
+    w[0] = 0.25; w[1] = 0.5; w[2] = 0.25;
+    return 3;
+  }
+  if (I == 0) {
+    idx[0] = 0; idx[1] = 1; idx[2] = 2;
+    w[0] = 0.5; w[1] = 0.375; w[2] = 0.125;
+    return 3;
+  }
+  if (I == nc - 1) {
+    idx[0] = 2 * I - 1; idx[1] = 2 * I; idx[2] = 2 * I + 1;
+    w[0] = 0.125; w[1] = 0.375; w[2] = 0.5;
+    return 3;
+  }
+  idx[0] = 2 * I - 1; idx[1] = 2 * I; idx[2] = 2 * I + 1; idx[3] = 2 * I + 2;
+  w[0] = 0.125; w[1] = 0.375; w[2] = 0.375; w[3] = 0.125;
+  return 4;
+}
+
+// Interpolation taps for fine index f (IGO.h:101-113, scatter stencils turned into
+// gathers): vertex f even -> c(f/2), odd -> (c(f/2) + c(f/2+1))/2; cell f=0 -> c(0),
+// f=2nc-1 -> c(nc-1), f=2I -> 3/4 c(I) + 1/4 c(I-1), f=2I+1 -> 3/4 c(I) + 1/4 c(I+1).
+__device__ __forceinline__ int interp_taps(int f, int nc, int cell, int* idx, double* w) {
+  if (!cell) {
+    if ((f & 1) == 0) {
+      idx[0] = f >> 1; w[0] = 1.0;
+      return 1;
+    }
+    idx[0] = f >> 1; idx[1] = (f >> 1) + 1;
+    w[0] = 0.5; w[1] = 0.5;
+    return 2;
+  }
+  const int I = f >> 1;
+  if (f == 0 || f == 2 * nc - 1) {
+    idx[0] = I; w[0] = 1.0;
+    return 1;
+  }
+  idx[0] = I; w[0] = 0.75;
+  idx[1] = (f & 1) ? I + 1 : I - 1; w[1] = 0.25;
+  return 2;
+}
+
+// coarse(I,J,K) = sum w_x w_y w_z fine(...)   (fine: g level geometry, may read ghosts)
+template <typename T, typename A, int DIM>
+__global__ void __launch_bounds__(256) restrict_k(const T* __restrict__ fine, Geo gf,
+                                                  T* __restrict__ coarse, Geo gc, int cx, int cy,
+                                                  int cz, int fz_shift) {
+  const int K = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int J = blockIdx.y * blockDim.y + threadIdx.y;
+  const int I = blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= gc.nx || J >= gc.ny) return;
+  int ix[4], iy[4], iz[4];
+  double wx[4], wy[4], wz[4];
+  const int nxn = restrict_taps(I, gc.nx, cx, ix, wx);
+  const int nyn = restrict_taps(J, gc.ny, cy, iy, wy);
+  int nzn = 1;
+  iz[0] = 0; wz[0] = 1.0;
+  if (DIM == 3) nzn = restrict_taps(K, gc.nz, cz, iz, wz);
+  A v = A(0);
+  for (int c = 0; c < nzn; ++c)
+    for (int bq = 0; bq < nyn; ++bq)
+      for (int a = 0; a < nxn; ++a) {
+        const int64_t q = ix[a] + gf.sy * iy[bq] + gf.sz * (int64_t)(iz[c] - fz_shift);
+        v += (A)(wx[a] * wy[bq] * wz[c]) * (A)fine[q];
+      }
+  coarse[I + gc.sy * J + gc.sz * K] = (T)v;
+}
+
+// fine(i,j,k) (+)= sum w coarse(...)
+template <typename T, int DIM, int ADD>
+__global__ void __launch_bounds__(256) interp_k(const T* __restrict__ coarse, Geo gc,
+                                                T* __restrict__ fine, Geo gf, int cx, int cy,
+                                                int cz) {
+  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= gf.nx || j >= gf.ny) return;
+  int ix[2], iy[2], iz[2];
+  double wx[2], wy[2], wz[2];
+  const int nxn = interp_taps(i, gc.nx, cx, ix, wx);
+  const int nyn = interp_taps(j, gc.ny, cy, iy, wy);
+  int nzn = 1;
+  iz[0] = 0; wz[0] = 1.0;
+  if (DIM == 3) nzn = interp_taps(k, gc.nz, cz, iz, wz);
+  T v = T(0);
+  for (int c = 0; c < nzn; ++c)
+    for (int bq = 0; bq < nyn; ++bq)
+      for (int a = 0; a < nxn; ++a)
+        v += (T)(wx[a] * wy[bq] * wz[c]) * coarse[ix[a] + gc.sy * iy[bq] + gc.sz * iz[c]];
+  const int64_t p = i + gf.sy * j + gf.sz * k;
+  if (ADD) fine[p] += v;
+  else fine[p] = v;
+}
+
+// 3D slab versions: z taps are computed from GLOBAL plane indices (zoff) and the
+// global coarse depth ncz; local plane -1 / nz are the ghost planes (filled by the
+// halo exchange before the launch).  On one GPU zoff = 0 and the slab is the grid.
+template <typename T, typename A>
+__global__ void __launch_bounds__(256) restrict_slab_k(const T* __restrict__ fine, Geo gf,
+                                                       T* __restrict__ coarse, Geo gc, int cx,
+                                                       int cy, int cz, int fz_shift, int ncz) {
+  const int K = blockIdx.z;
+  const int J = blockIdx.y * blockDim.y + threadIdx.y;
+  const int I = blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= gc.nx || J >= gc.ny) return;
+  int ix[4], iy[4], iz[4];
+  double wx[4], wy[4], wz[4];
+  const int nxn = restrict_taps(I, gc.nx, cx, ix, wx);
+  const int nyn = restrict_taps(J, gc.ny, cy, iy, wy);
+  const int nzn = restrict_taps(K + gc.zoff, ncz, cz, iz, wz);
+  A v = A(0);
+  for (int c = 0; c < nzn; ++c)
+    for (int bq = 0; bq < nyn; ++bq)
+      for (int a = 0; a < nxn; ++a) {
+        const int64_t q = ix[a] + gf.sy * iy[bq] + gf.sz * (int64_t)(iz[c] - fz_shift);
+        v += (A)(wx[a] * wy[bq] * wz[c]) * (A)fine[q];
+      }
+  coarse[I + gc.sy * J + gc.sz * K] = (T)v;
+}
+
+template <typename T, int ADD>
+__global__ void __launch_bounds__(256) interp_slab_k(const T* __restrict__ coarse, Geo gc,
+                                                     T* __restrict__ fine, Geo gf, int cx, int cy,
+                                                     int cz, int ncz) {
+  const int k = blockIdx.z;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= gf.nx || j >= gf.ny) return;
+  int ix[2], iy[2], iz[2];
+  double wx[2], wy[2], wz[2];
+  const int nxn = interp_taps(i, gc.nx, cx, ix, wx);
+  const int nyn = interp_taps(j, gc.ny, cy, iy, wy);
+  const int nzn = interp_taps(k + gf.zoff, ncz, cz, iz, wz);
+  T v = T(0);
+  for (int c = 0; c < nzn; ++c)
+    for (int bq = 0; bq < nyn; ++bq)
+      for (int a = 0; a < nxn; ++a)
+        v += (T)(wx[a] * wy[bq] * wz[c]) *
+             coarse[ix[a] + gc.sy * iy[bq] + gc.sz * (int64_t)(iz[c] - gc.zoff)];
+  const int64_t p = i + gf.sy * j + gf.sz * k;
+  if (ADD) fine[p] += v;
+  else fine[p] = v;
+}
+
+// ---------------------------------------------------------------------------
+// coarsest-grid solve x = A^-1 b with the precomputed fp64 inverse: one wave per row
+template <typename T>
+__global__ void __launch_bounds__(256) coarse_solve_k(const double* __restrict__ inv,
+                                                      const T* __restrict__ b, T* __restrict__ x,
+                                                      int n) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const double* a = inv + (int64_t)row * n;
+  double s = 0.0;
+  for (int c = lane; c < n; c += 64) s += a[c] * (double)b[c];
+  s = wave_sum(s);
+  if (lane == 0) x[row] = (T)s;
+}
+
+// ---------------------------------------------------------------------------
+// elementwise helpers
+template <typename T>
+__global__ void __launch_bounds__(256) fill_k(T* __restrict__ x, int64_t n, T v) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x)
+    x[q] = v;
+}
+
+template <typename S, typename D>
+__global__ void __launch_bounds__(256) convert_k(const S* __restrict__ x, D* __restrict__ y,
+                                                 int64_t n) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x)
+    y[q] = (D)x[q];
+}
+
+// static_cast<OutputPixelType>(double) for integer outputs: truncation toward zero,
+// saturated to the type's range (the reference leaves out-of-range values undefined)
+template <typename S, typename D>
+__global__ void __launch_bounds__(256) convert_int_k(const S* __restrict__ x, D* __restrict__ y,
+                                                     int64_t n, double lo, double hi) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    double v = trunc((double)x[q]);
+    v = v < lo ? lo : (v > hi ? hi : v);
+    if (v != v) v = 0.0;
+    y[q] = (D)v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// setup (fp64): AoS input tensor -> SoA, kind detection, coefficient fields
+template <typename S>
+__global__ void __launch_bounds__(256) aos_to_soa_k(const S* __restrict__ in, double* __restrict__ out,
+                                                    int64_t n, int ncomp) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x)
+    for (int c = 0; c < ncomp; ++c) out[c * n + q] = (double)in[q * ncomp + c];
+}
+
+// flags[0] += any off-diagonal != 0, flags[1] += any diagonal entries differ
+__global__ void __launch_bounds__(256) tensor_kind_k(const double* __restrict__ M, int64_t n, int dim,
+                                                     unsigned int* __restrict__ flags) {
+  unsigned int off = 0, aniso = 0;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    if (dim == 3) {
+      off |= (M[1 * n + q] != 0.0) | (M[2 * n + q] != 0.0) | (M[4 * n + q] != 0.0);
+      aniso |= (M[0 * n + q] != M[3 * n + q]) | (M[0 * n + q] != M[5 * n + q]);
+    } else {
+      off |= (M[1 * n + q] != 0.0);
+      aniso |= (M[0 * n + q] != M[2 * n + q]);
+    }
+  }
+  if (__any(off) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
+  if (__any(aniso) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1u);
+}
+
+__device__ __forceinline__ int tcomp(int dim, int d, int d2) {
+  if (d > d2) { const int t = d; d = d2; d2 = t; }
+  return d * dim - d * (d - 1) / 2 + (d2 - d);
+}
+
+// 2h * d f / dx_d with the reference's border formulas (GH.hxx:447-474)
+__device__ __forceinline__ double delta_f(const double* __restrict__ f, int64_t p, int idx, int n,
+                                          int64_t st) {
+  if (idx == 0) return -3. * f[p] + 4. * f[p + st] - 1. * f[p + 2 * st];
+  if (n - idx == 1) return 3. * f[p] - 4. * f[p - st] + 1. * f[p - 2 * st];
+  return f[p + st] - f[p - st];
+}
+
+// coefficient fields of one (global) level from its fp64 tensor
+template <typename T, int DIM, int KIND>
+__global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M, int nx, int ny,
+                                                    int nz, double hx, double hy, double hz,
+                                                    double dt, T* __restrict__ cf) {
+  using L = CoefLayout<DIM, KIND>;
+  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nx || j >= ny) return;
+  const int64_t n = (int64_t)nx * ny * nz;
+  const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
+  const double h[3] = {hx, hy, hz};
+  const int nn[3] = {nx, ny, nz};
+  const int id[3] = {i, j, k};
+  const int64_t st[3] = {1, nx, (int64_t)nx * ny};
+  if (KIND == KISO) {
+    cf[p] = (T)(dt * M[p] / (h[0] * h[0]));
+  } else {
+    for (int d = 0; d < DIM; ++d) cf[d * n + p] = (T)(dt * M[tcomp(DIM, d, d) * n + p] / (h[d] * h[d]));
+  }
+  for (int d = 0; d < DIM; ++d) {
+    double s = 0.0;
+    for (int d2 = 0; d2 < DIM; ++d2)
+      s += delta_f(M + tcomp(DIM, d, d2) * n, p, id[d2], nn[d2], st[d2]) / (2.0 * h[d2]);
+    cf[(L::NA + d) * n + p] = (T)(dt / (2.0 * h[d]) * s);
+  }
+  if (KIND == KFULL) {
+    int e = L::NA + L::NG;
+    for (int d = 0; d < DIM; ++d)
+      for (int d2 = d + 1; d2 < DIM; ++d2, ++e)
+        cf[e * n + p] = (T)(dt * M[tcomp(DIM, d, d2) * n + p] / (2.0 * h[d] * h[d2]));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// deterministic synthetic inputs (bench / smoke), mirrored in tests/synth.py
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ double u01(uint64_t seed, int64_t q) {
+  return (double)(splitmix64(seed * 0x100000001B3ull + (uint64_t)q) >> 11) * 0x1.0p-53;
+}
+
+// x-fastest global index q over the global grid, written at local plane offset
+template <typename T>
+__global__ void __launch_bounds__(256) synth_image_k(T* __restrict__ x, Geo g, int64_t nxg,
+                                                     int64_t nyg, uint64_t seed) {
+  const int k = blockIdx.z;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.nx || j >= g.ny) return;
+  const int64_t qg = i + nxg * (j + nyg * (int64_t)(k + g.zoff));
+  x[i + g.sy * j + g.sz * k] = (T)u01(seed, qg);
+}
+
+// VED-form tensor T = lp I + (la - lp) v v^T (include/itkVEDMultigridImageFilter.hxx:327-365
+// with V = resp^(1/s), identity where V == 0) on the analytic fields of tests/synth.py
+__global__ void __launch_bounds__(256) synth_ved_k(double* __restrict__ M, int nx, int ny, int nz,
+                                                   uint64_t seed, double eps, double omega,
+                                                   double sens) {
+  const int k = blockIdx.z;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nx || j >= ny) return;
+  const int64_t n = (int64_t)nx * ny * nz;
+  const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
+  const double PI2 = 6.283185307179586;
+  const double x = i, y = j, z = k;
+  const double fx = nx > 2 ? nx : 2, fy = ny > 2 ? ny : 2, fz = nz > 2 ? nz : 2;
+  const double sd = (double)seed;
+  double s = sin(PI2 * x / fx * 3.0 + sd) * sin(PI2 * y / fy * 2.0 + 0.5 * sd) *
+             cos(PI2 * z / fz * 2.5);
+  s = s > 0.0 ? s : 0.0;
+  const double resp = s * s;
+  const double V = resp > 0.0 ? pow(resp, 1.0 / sens) : 0.0;
+  double vx = sin(PI2 * y / fy * 1.5) + 0.3;
+  double vy = cos(PI2 * z / fz * 1.25);
+  double vz = 1.0 + 0.5 * sin(PI2 * x / fx);
+  const double nrm = sqrt(vx * vx + vy * vy + vz * vz);
+  vx /= nrm; vy /= nrm; vz /= nrm;
+  const double lp = 1.0 + (eps - 1.0) * V;
+  const double la = 1.0 + (omega - 1.0) * V;
+  const double d = la - lp;
+  M[0 * n + p] = lp + d * vx * vx;
+  M[1 * n + p] = d * vx * vy;
+  M[2 * n + p] = d * vx * vz;
+  M[3 * n + p] = lp + d * vy * vy;
+  M[4 * n + p] = d * vy * vz;
+  M[5 * n + p] = lp + d * vz * vz;
+}
+
+// isotropic c(x) I, c = 1 + 0.5 sin sin sin (period 32)
+__global__ void __launch_bounds__(256) synth_iso_k(double* __restrict__ M, int nx, int ny, int nz,
+                                                   int dim, uint64_t seed) {
+  const int k = blockIdx.z;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nx || j >= ny) return;
+  const int64_t n = (int64_t)nx * ny * nz;
+  const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
+  const double PI2 = 6.283185307179586;
+  const double ph = 0.3 * (double)seed;
+  double c = sin(PI2 * i / 32.0 + ph) * sin(PI2 * j / 32.0 + ph);
+  if (dim == 3) c *= sin(PI2 * k / 32.0 + ph);
+  c = 1.0 + 0.5 * c;
+  if (dim == 3) {
+    M[0 * n + p] = c; M[1 * n + p] = 0.0; M[2 * n + p] = 0.0;
+    M[3 * n + p] = c; M[4 * n + p] = 0.0; M[5 * n + p] = c;
+  } else {
+    M[0 * n + p] = c; M[1 * n + p] = 0.0; M[2 * n + p] = c;
+  }
+}
+
+}  // namespace mad

@@ -1,0 +1,233 @@
+"""Host-side mirror of the reference's operator surface over the C ABI.
+
+``Solver`` exposes the kernel-level entry points of include/mad.h (one
+context = hierarchy + operators resident on one GPU); the ITK-shaped filter
+classes live in ``filters.py``.  numpy arrays use (z, y, x) / (y, x) order;
+the C ABI takes sizes and spacings x first, as ITK does.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _capi as C
+
+_DT = {np.dtype(np.uint8): C.U8, np.dtype(np.int8): C.I8, np.dtype(np.uint16): C.U16,
+       np.dtype(np.int16): C.I16, np.dtype(np.uint32): C.U32, np.dtype(np.int32): C.I32,
+       np.dtype(np.float32): C.F32, np.dtype(np.float64): C.F64}
+
+
+def mad_dtype(dt):
+    dt = np.dtype(dt)
+    if dt not in _DT:
+        raise TypeError(f"unsupported pixel type {dt}")
+    return _DT[dt]
+
+
+def max_depth(shape):
+    """GridsHierarchy depth rule (include/mad/itkGridsHierarchy.hxx:36-59)."""
+    dim = len(shape)
+    n = (ctypes.c_int64 * 3)(*(list(reversed(shape)) + [1] * (3 - dim)))
+    return C.load().mad_max_depth(dim, n)
+
+
+def slab_range(nz, nranks, rank, align=1):
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    C.check(C.load().mad_slab_range(nz, nranks, rank, align, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def tensor_to_aos(tensor, shape):
+    """Accept (ncomp, *shape) SoA or (*shape, ncomp) AoS; return contiguous AoS."""
+    t = np.asarray(tensor)
+    dim = len(shape)
+    ncomp = dim * (dim + 1) // 2
+    if t.shape == (ncomp,) + tuple(shape):
+        t = np.moveaxis(t, 0, -1)
+    elif t.shape != tuple(shape) + (ncomp,):
+        raise ValueError(f"tensor shape {t.shape} does not match image {shape} "
+                         f"(expected {(ncomp,) + tuple(shape)} or {tuple(shape) + (ncomp,)})")
+    if t.dtype not in (np.float32, np.float64):
+        t = t.astype(np.float64)
+    return np.ascontiguousarray(t)
+
+
+class Solver:
+    """One GPU context (mad_ctx).  Parameters mirror the filter setters
+    (itkMultigridAnisotropicDiffusionImageFilter.h:133-160) and their defaults."""
+
+    def __init__(self, shape, spacing=None, *, time_step=0.01, cycle=C.VCYCLE,
+                 smoother=C.GAUSS_SEIDEL, iterations_per_grid=2, max_cycles=100,
+                 number_of_steps=1, tolerance=1e-6, omega=2.0 / 3.0, verbose=False,
+                 precision=C.FP32, stall_guard=None, device=-1, tensor_kind=C.TENSOR_AUTO,
+                 nranks=1, rank=0, global_shape=None):
+        L = C.load()
+        self.shape = tuple(int(s) for s in shape)  # this rank's slab
+        gshape = tuple(global_shape) if global_shape is not None else self.shape
+        self.dim = len(gshape)
+        if self.dim not in (2, 3):
+            raise ValueError("images must be 2D or 3D")
+        d = C.default_desc()
+        d.dim = self.dim
+        size = list(reversed(gshape)) + [1] * (3 - self.dim)
+        for q in range(3):
+            d.size[q] = size[q]
+        sp = list(spacing) if spacing is not None else [1.0] * self.dim
+        for q in range(3):
+            d.spacing[q] = sp[q] if q < self.dim else 1.0
+        d.cycle = int(cycle)
+        d.smoother = int(smoother)
+        d.iterations_per_grid = int(iterations_per_grid)
+        d.max_cycles = int(max_cycles)
+        d.number_of_steps = int(number_of_steps)
+        d.time_step = float(time_step)
+        d.tolerance = float(tolerance)
+        d.omega = float(omega)
+        d.verbose = int(bool(verbose))
+        d.precision = int(precision)
+        d.stall_guard = int(precision == C.FP32) if stall_guard is None else int(stall_guard)
+        d.device = int(device)
+        d.tensor_kind = int(tensor_kind)
+        d.nranks = int(nranks)
+        d.rank = int(rank)
+        self._desc = d
+        ctx = ctypes.c_void_p()
+        C.check(L.mad_create(ctypes.byref(d), ctypes.byref(ctx)))
+        self._ctx = ctx
+        self._L = L
+        self.precision = precision
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.mad_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        return C.check(rc, self._ctx)
+
+    # ------------------------------------------------------------ setup
+    def set_tensor(self, tensor):
+        """SetDiffusionTensor: (ncomp, *shape) SoA or (*shape, ncomp) AoS, ITK order."""
+        gshape = tuple(reversed([self._desc.size[q] for q in range(self.dim)]))
+        t = tensor_to_aos(tensor, gshape)
+        self._check(self._L.mad_set_tensor(self._ctx, t.ctypes.data_as(ctypes.c_void_p),
+                                           C.F64 if t.dtype == np.float64 else C.F32))
+
+    def synth_tensor(self, kind=0, seed=4):
+        self._check(self._L.mad_bench_synth_tensor(self._ctx, kind, seed))
+
+    def comm_init(self, uid):
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        self._check(self._L.mad_comm_init(self._ctx, buf))
+
+    def setup(self):
+        self._check(self._L.mad_setup(self._ctx))
+
+    @property
+    def num_levels(self):
+        return self._L.mad_num_levels(self._ctx)
+
+    def level_info(self, level):
+        n = (ctypes.c_int64 * 3)()
+        h = (ctypes.c_double * 3)()
+        c = (ctypes.c_int32 * 3)()
+        self._check(self._L.mad_level_info(self._ctx, level, n, h, c))
+        return dict(shape=tuple(reversed(list(n)[: self.dim])), spacing=list(h)[: self.dim],
+                    centering=list(c)[: self.dim])
+
+    def shape_at(self, level):
+        return self.level_info(level)["shape"]
+
+    # ------------------------------------------------------------ kernel level
+    def upload(self, level, which, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        if a.shape != self.shape_at(level):
+            raise ValueError(f"level {level} array must have shape {self.shape_at(level)}")
+        self._check(self._L.mad_upload(self._ctx, level, which,
+                                       a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+
+    def download(self, level, which):
+        a = np.empty(self.shape_at(level), dtype=np.float64)
+        self._check(self._L.mad_download(self._ctx, level, which,
+                                         a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        return a
+
+    def fill(self, level, which, value):
+        self._check(self._L.mad_fill(self._ctx, level, which, float(value)))
+
+    def smooth(self, level, sweeps=1):
+        self._check(self._L.mad_smooth(self._ctx, level, sweeps))
+
+    def residual(self, level):
+        v = ctypes.c_double()
+        self._check(self._L.mad_residual(self._ctx, level, ctypes.byref(v)))
+        return v.value
+
+    def norm(self, level, which):
+        v = ctypes.c_double()
+        self._check(self._L.mad_norm(self._ctx, level, which, ctypes.byref(v)))
+        return v.value
+
+    def restrict(self, level):
+        self._check(self._L.mad_restrict(self._ctx, level))
+
+    def interpolate(self, level):
+        self._check(self._L.mad_interpolate(self._ctx, level))
+
+    def prolongate_add(self, level):
+        self._check(self._L.mad_prolongate_add(self._ctx, level))
+
+    def coarse_solve(self):
+        self._check(self._L.mad_coarse_solve(self._ctx))
+
+    def vcycle(self):
+        self._check(self._L.mad_vcycle(self._ctx))
+
+    def fmg(self):
+        self._check(self._L.mad_fmg(self._ctx))
+
+    def synchronize(self):
+        self._check(self._L.mad_synchronize(self._ctx))
+
+    def synth_level(self, level, which, seed):
+        self._check(self._L.mad_bench_synth_level(self._ctx, level, which, seed))
+
+    # ------------------------------------------------------------ filter
+    def run(self, image, out_dtype=np.float32):
+        """GenerateData on a host image (numpy); returns (output, stats dict)."""
+        img = np.ascontiguousarray(image)
+        if img.shape != self.shape:
+            raise ValueError(f"image shape {img.shape} != {self.shape}")
+        out = np.empty(self.shape, dtype=out_dtype)
+        st = C.MadStats()
+        self._check(self._L.mad_run(self._ctx, img.ctypes.data_as(ctypes.c_void_p),
+                                    mad_dtype(img.dtype), out.ctypes.data_as(ctypes.c_void_p),
+                                    mad_dtype(out_dtype), ctypes.byref(st)))
+        stats = st.as_dict()
+        stats["step_cycles"], stats["step_relres"] = [], []
+        for s in range(st.steps):
+            cy, rr = ctypes.c_uint32(), ctypes.c_double()
+            self._check(self._L.mad_get_step_stats(self._ctx, s, ctypes.byref(cy),
+                                                   ctypes.byref(rr)))
+            stats["step_cycles"].append(cy.value)
+            stats["step_relres"].append(rr.value)
+        return out, stats
+
+    def bench_smooth(self, level, sweeps):
+        t, k, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
+        self._check(self._L.mad_bench_smooth(self._ctx, level, sweeps, ctypes.byref(t),
+                                             ctypes.byref(k), ctypes.byref(n)))
+        return t.value, k.value, n.value
+
+    def bench_vcycle(self, cycles):
+        t = ctypes.c_double()
+        self._check(self._L.mad_bench_vcycle(self._ctx, cycles, ctypes.byref(t)))
+        return t.value
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    C.check(C.load().mad_comm_unique_id(buf))
+    return buf.raw

@@ -1,0 +1,169 @@
+"""Per-kernel parity of the HIP path (through the C ABI) against the fp64
+oracle's golden fixtures, in fp32 and fp64.
+
+Tolerances
+  fp64: max|gpu - ref| <= 1e-12 * max|ref| (single kernels), 1e-10 (cycles).
+  fp32: single stencil kernels are checked pointwise against the rounding bound
+        |gpu - ref| <= 16 eps32 * (|b| + D|x| + sum |coef| |x_nb|)
+        (inputs and coefficients are rounded to fp32 once, ~20 fused ops);
+        transfers 4 eps32 relative; composite cycles 2e-5 of max|ref|.
+"""
+import numpy as np
+import pytest
+
+import mf_numpy as mf
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+EPS32 = np.finfo(np.float32).eps
+CASES = ["k2d_cell", "k2d_vert", "k3d_vert", "k3d_cell", "k3d_mixed", "k3d_diag", "k3d_iso",
+         "k3d_deep", "k2d_deep"]
+
+
+def solver(g, precision, smoother):
+    import multigridanisotropicdiffusion_amd as M
+    shape = tuple(int(s) for s in g["shape"])
+    s = M.Solver(shape, tuple(g["spacing"]), time_step=float(g["dt"]), smoother=smoother,
+                 precision=precision)
+    s.set_tensor(g["tensor"])
+    s.setup()
+    return s
+
+
+def relmax(a, ref):
+    return np.abs(a - ref).max() / max(np.abs(ref).max(), 1e-300)
+
+
+def stencil_mag(g, x, b):
+    co = mf.coefficients(g["tensor"], tuple(g["spacing"]), float(g["dt"]))
+    aco = dict(a=[np.abs(v) for v in co["a"]], g=[np.abs(v) for v in co["g"]],
+               e={k: np.abs(v) for k, v in co["e"].items()})
+    # |a+g| + |a-g| <= 2(|a| + |g|): the off-sum of |x| with |coefficients| doubled bounds it
+    return np.abs(b) + mf.diag(co) * np.abs(x) + 2.0 * mf.off_sum(np.abs(x), aco)
+
+
+@pytest.fixture(params=["fp32", "fp64"])
+def prec(request):
+    import multigridanisotropicdiffusion_amd as M
+    return M.FP32 if request.param == "fp32" else M.FP64
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_wj_sweep_and_residual(name, prec):
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    s = solver(g, prec, M.WEIGHTED_JACOBI)
+    x, b = g["x"], g["b"]
+    s.upload(0, M.capi.X, x)
+    s.upload(0, M.capi.B, b)
+    nrm = s.residual(0)
+    r = s.download(0, M.capi.R)
+    s.smooth(0, 1)
+    wj = s.download(0, M.capi.X)
+    if prec == M.FP64:
+        assert relmax(r, g["residual"]) < 1e-12
+        assert relmax(wj, g["wj"]) < 1e-12
+        assert abs(nrm - np.linalg.norm(g["residual"])) < 1e-12 * np.linalg.norm(g["residual"])
+    else:
+        mag = stencil_mag(g, x, b)
+        assert (np.abs(r - g["residual"]) / mag).max() < 16 * EPS32
+        assert (np.abs(wj - g["wj"]) / (mag / mf.diag(mf.coefficients(
+            g["tensor"], tuple(g["spacing"]), float(g["dt"]))) + np.abs(x))).max() < 16 * EPS32
+        assert abs(nrm - np.linalg.norm(r)) < 1e-6 * np.linalg.norm(r)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gs_colour_sweep(name, prec):
+    """Multicolour GS: 4 colours for the 9/19-point full-tensor operator, red-black for
+    diagonal/isotropic tensors -- one sweep equals the oracle's multicolour sweep."""
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    s = solver(g, prec, M.GAUSS_SEIDEL)
+    s.upload(0, M.capi.X, g["x"])
+    s.upload(0, M.capi.B, g["b"])
+    s.smooth(0, 1)
+    out = s.download(0, M.capi.X)
+    assert relmax(out, g["gs_color"]) < (1e-12 if prec == M.FP64 else 64 * EPS32)
+
+
+@pytest.mark.parametrize("name", ["k2d_cell", "k2d_vert", "k3d_vert", "k3d_mixed", "k3d_diag"])
+def test_gs_lexicographic_sweep(name, prec):
+    """Hyperplane-wavefront GS reproduces the reference's lexicographic sweep
+    (include/mad/itkMultigridGaussSeidelSmoother.hxx:67-106) per sweep."""
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    s = solver(g, prec, M.GAUSS_SEIDEL_LEX)
+    s.upload(0, M.capi.X, g["x"])
+    s.upload(0, M.capi.B, g["b"])
+    s.smooth(0, 1)
+    out = s.download(0, M.capi.X)
+    assert relmax(out, g["gs_lex"]) < (1e-12 if prec == M.FP64 else 64 * EPS32)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_transfers_and_coarse_solve(name, prec):
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    s = solver(g, prec, M.GAUSS_SEIDEL)
+    tol = 1e-14 if prec == M.FP64 else 4 * EPS32
+    if "restrict" in g:
+        s.upload(0, M.capi.R, g["residual"])
+        s.restrict(0)
+        assert relmax(s.download(1, M.capi.B), g["restrict"]) < tol
+        s.upload(1, M.capi.X, g["xc"])
+        s.interpolate(0)
+        assert relmax(s.download(0, M.capi.X), g["interp"]) < tol
+        s.upload(0, M.capi.X, g["x"])
+        s.prolongate_add(0)
+        assert relmax(s.download(0, M.capi.X), g["x"] + g["interp"]) < tol
+    L = s.num_levels - 1
+    s.upload(L, M.capi.B, g["bc"])
+    s.coarse_solve()
+    out = s.download(L, M.capi.X)
+    assert relmax(out, g["coarse_solve"]) < (1e-12 if prec == M.FP64 else 1e-5)
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("smoother_key", ["wj", "gs_color", "gs_lex"])
+def test_vcycle(name, prec, smoother_key):
+    """One V-cycle (itkMultigridAnisotropicDiffusionImageFilter.hxx:341-493) with the
+    same smoother as the oracle's."""
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    sm = {"wj": M.WEIGHTED_JACOBI, "gs_color": M.GAUSS_SEIDEL, "gs_lex": M.GAUSS_SEIDEL_LEX}[smoother_key]
+    if sm == M.GAUSS_SEIDEL_LEX and name in ("k3d_deep", "k2d_deep", "k3d_cell", "k3d_iso"):
+        pytest.skip("lexicographic mode covered on the smaller cases")
+    s = solver(g, prec, sm)
+    s.upload(0, M.capi.X, g["x"])
+    s.upload(0, M.capi.B, g["b"])
+    s.vcycle()
+    out = s.download(0, M.capi.X)
+    assert relmax(out, g["vcycle_" + smoother_key]) < (1e-10 if prec == M.FP64 else 2e-5)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_fmg(name, prec):
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    s = solver(g, prec, M.WEIGHTED_JACOBI)
+    s.upload(0, M.capi.B, g["b"])
+    s.fmg()
+    out = s.download(0, M.capi.X)
+    assert relmax(out, g["fmg_wj"]) < (1e-10 if prec == M.FP64 else 2e-5)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_converged_solution_matches_reference_gs(name, prec):
+    """End-to-end: the GPU multicolour-GS V-cycle solve converges to the reference
+    (lexicographic GS) solution: ||u_gpu - u_ref||_inf / ||u_ref||_inf <= 1e-5 (fp32),
+    1e-9 (fp64)."""
+    import multigridanisotropicdiffusion_amd as M
+    g = load_golden(name)
+    shape = tuple(int(v) for v in g["shape"])
+    s = M.Solver(shape, tuple(g["spacing"]), time_step=float(g["dt"]), precision=prec,
+                 tolerance=1e-11 if prec == M.FP64 else 1e-7)
+    s.set_tensor(g["tensor"])
+    out, st = s.run(g["b"], out_dtype=np.float64)
+    assert relmax(out, g["run_gs_lex"]) < (1e-9 if prec == M.FP64 else 1e-5)
+    assert st["last_relres"] < (1e-11 if prec == M.FP64 else 1e-5)
