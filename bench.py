@@ -34,6 +34,7 @@ def parse():
     p.add_argument("--size", type=int, default=512)
     p.add_argument("--vcycles", type=int, default=5)
     p.add_argument("--smoother", default="gs", choices=["gs", "wj"])
+    p.add_argument("--gs-kernel", type=int, default=0, help="0 auto (fused), 1 per-colour passes")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -93,7 +94,8 @@ def main():
     shape = (nz_local, S, S)
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
     s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
-                 nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape)
+                 nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
+                 gs_kernel=a.gs_kernel)
     if world > 1:
         import torch
         uid = M.comm_unique_id() if rank == 0 else bytes(128)
@@ -145,8 +147,9 @@ def main():
         if dist is not None:
             dist.barrier()
         return
-    # roofline of the dominant kernel: per launch one colour class = 1/ncolors of the slab
-    ncolors = 4 if a.smoother == "gs" else 1
+    # roofline of the dominant kernel: the fused GS sweep processes the whole slab per
+    # launch; the per-colour variant one colour class (1/4 of the slab) per launch
+    ncolors = 4 if (a.smoother == "gs" and a.gs_kernel == 1) else 1
     units_per_launch = float(shape[0] * shape[1] * shape[2]) / ncolors
     achieved = BYTES_PER_VOXEL_SMOOTH * units_per_launch / (kern_ms * 1e-3) / 1e9
     tag = f"{a.smoother}_{S}"
@@ -154,7 +157,8 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
             "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "kernel": "gs_color_k<float,3,FULL>" if a.smoother == "gs" else "wj_k<float,3,FULL>",
+            "kernel": ("gs_fused_k<float,FULL,64,16,512>" if a.gs_kernel != 1 else
+                       "gs_color_k<float,3,FULL>") if a.smoother == "gs" else "wj_k<float,3,FULL>",
             "kernel_ms_mean": round(kern_ms, 5), "launches": launches,
             "algorithmic_bytes_per_launch": BYTES_PER_VOXEL_SMOOTH * units_per_launch}
     if traffic:

@@ -99,7 +99,9 @@ typedef struct mad_desc {
   int32_t tensor_kind;           /* mad_tensor_kind, default AUTO */
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
   int32_t rank;                  /* this rank */
-  int32_t reserved[9];
+  int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep),
+                                    1 one launch per colour, 2 fused */
+  int32_t reserved[8];
 } mad_desc;
 
 typedef struct mad_stats {

@@ -61,7 +61,8 @@ class MadDesc(ctypes.Structure):
         ("tensor_kind", ctypes.c_int32),
         ("nranks", ctypes.c_int32),
         ("rank", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 9),
+        ("gs_kernel", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 8),
     ]
 
 

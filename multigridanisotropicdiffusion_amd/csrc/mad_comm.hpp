@@ -58,20 +58,22 @@ class Comm {
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
 
-  // a: base pointer of local plane 0; plane -1 and plane nz are ghosts
-  void exchange_planes(void* a, int64_t plane, int nz, int has_lo, int has_hi, size_t esz,
-                       bool is_double, hipStream_t s) {
+  // a: base pointer of local plane 0; planes -depth..-1 and nz..nz+depth-1 are ghosts.
+  // Sends the first / last `depth` owned planes to rank -+ 1 (one grouped call).
+  void exchange_planes(void* a, int64_t plane, int nz, int depth, int has_lo, int has_hi,
+                       size_t esz, bool is_double, hipStream_t s) {
     char* base = (char*)a;
     const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
     const size_t pb = (size_t)plane * esz;
+    const size_t cnt = (size_t)plane * depth;
     NCCL_CHECK(ncclGroupStart());
     if (has_lo) {
-      NCCL_CHECK(ncclSend(base, plane, dt, rank_ - 1, comm_, s));
-      NCCL_CHECK(ncclRecv(base - pb, plane, dt, rank_ - 1, comm_, s));
+      NCCL_CHECK(ncclSend(base, cnt, dt, rank_ - 1, comm_, s));
+      NCCL_CHECK(ncclRecv(base - depth * pb, cnt, dt, rank_ - 1, comm_, s));
     }
     if (has_hi) {
-      NCCL_CHECK(ncclSend(base + (size_t)(nz - 1) * pb, plane, dt, rank_ + 1, comm_, s));
-      NCCL_CHECK(ncclRecv(base + (size_t)nz * pb, plane, dt, rank_ + 1, comm_, s));
+      NCCL_CHECK(ncclSend(base + (size_t)(nz - depth) * pb, cnt, dt, rank_ + 1, comm_, s));
+      NCCL_CHECK(ncclRecv(base + (size_t)nz * pb, cnt, dt, rank_ + 1, comm_, s));
     }
     NCCL_CHECK(ncclGroupEnd());
   }

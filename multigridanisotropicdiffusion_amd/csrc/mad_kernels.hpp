@@ -38,16 +38,26 @@ inline int coef_count(int dim, int kind) {
 }
 
 // Geometry of one level slab as seen by a kernel.  Arrays are x-fastest; the
-// base pointer addresses local plane 0; in 3D one ghost plane is allocated on
-// each side (used for rank halos; at a global boundary the mirror is used).
+// base pointer addresses local plane 0; in 3D GHOST ghost planes are allocated on
+// each side (rank halos; at a global boundary the mirror is used instead).
+// Coefficient fields use an x-parity-split row layout: in every row the even-x
+// points come first, then the odd-x points (cidx below), so each colour class of
+// a row is one contiguous run.
+constexpr int GHOST = 4;
+
 struct Geo {
   int nx, ny, nz;       // local sizes
   int zoff;             // global z index of local plane 0 (colour parity)
-  int zlo_ghost;        // 1: plane -1 holds the lower neighbour's data
-  int zhi_ghost;        // 1: plane nz holds the upper neighbour's data
+  int zlo_ghost;        // 1: planes -GHOST..-1 hold the lower neighbour's data
+  int zhi_ghost;        // 1: planes nz..nz+GHOST-1 hold the upper neighbour's data
+  int hx0;              // (nx + 1) / 2: start of the odd-x half of a coefficient row
   int64_t sy, sz;       // strides
   int64_t N;            // nx*ny*nz (coefficient field stride)
 };
+
+__device__ __forceinline__ int64_t cidx(const Geo& g, int i, int j, int k) {
+  return (int64_t)k * g.sz + (int64_t)j * g.sy + ((i & 1) ? g.hx0 + (i >> 1) : (i >> 1));
+}
 
 template <typename T>
 struct Rat {
@@ -56,53 +66,101 @@ struct Rat {
 
 // ---------------------------------------------------------------------------
 // the per-point stencil: D and S of (A u)(p) = D u(p) - S(p)
+template <typename T>
+struct Coefs {
+  T ax, ay, az, gx, gy, gz, exy, exz, eyz;
+};
+
 template <typename T, int DIM, int KIND>
-__device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* __restrict__ cf,
-                                              const Geo& g, const Rat<T>& rat, int i, int j,
-                                              int k, int64_t p, T& D, T& S) {
-  using L = CoefLayout<DIM, KIND>;
-  const int64_t N = g.N;
-  const int64_t dxm = (i == 0) ? 1 : -1;
-  const int64_t dxp = (i == g.nx - 1) ? -1 : 1;
-  const int64_t dym = (j == 0) ? g.sy : -g.sy;
-  const int64_t dyp = (j == g.ny - 1) ? -g.sy : g.sy;
-  T ax, ay, az = T(0);
-  if (KIND == KISO) {
-    const T a = cf[p];
-    ax = a;
-    ay = a * rat.r[1];
-    if (DIM == 3) az = a * rat.r[2];
-  } else {
-    ax = cf[p];
-    ay = cf[N + p];
-    if (DIM == 3) az = cf[2 * N + p];
-  }
-  const T gx = cf[L::NA * N + p];
-  const T gy = cf[(L::NA + 1) * N + p];
-  T s = (ax + gx) * u[p + dxp] + (ax - gx) * u[p + dxm] + (ay + gy) * u[p + dyp] +
-        (ay - gy) * u[p + dym];
-  T d = T(1) + T(2) * (ax + ay);
-  int64_t dzm = 0, dzp = 0;
+__device__ __forceinline__ void coefs_from_raw(const T* raw, const Rat<T>& rat, Coefs<T>& q);
+
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void load_coefs(const T* __restrict__ cf, int64_t N, int64_t c,
+                                           const Rat<T>& rat, Coefs<T>& q) {
+  constexpr int NCF = CoefLayout<DIM, KIND>::N;
+  T raw[NCF];
+#pragma unroll
+  for (int a = 0; a < NCF; ++a) raw[a] = cf[a * N + c];
+  coefs_from_raw<T, DIM, KIND>(raw, rat, q);
+}
+
+// Neighbour values in a fixed order, mirror-resolved by the caller:
+//  0 xp  1 xm  2 yp  3 ym  4 zp  5 zm
+//  6 xp,yp  7 xp,ym  8 xm,yp  9 xm,ym   10 xp,zp 11 xp,zm 12 xm,zp 13 xm,zm
+// 14 yp,zp 15 yp,zm 16 ym,zp 17 ym,zm
+// Every smoother / residual kernel evaluates the operator through this one
+// function, so the fused and the per-colour GS kernels are bit-identical.
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void stencil_combine(const Coefs<T>& q, const T* nb, T& D, T& S) {
+  T s = (q.ax + q.gx) * nb[0] + (q.ax - q.gx) * nb[1] + (q.ay + q.gy) * nb[2] +
+        (q.ay - q.gy) * nb[3];
+  T d = T(1) + T(2) * (q.ax + q.ay);
   if (DIM == 3) {
-    dzm = (k == 0 && !g.zlo_ghost) ? g.sz : -g.sz;
-    dzp = (k == g.nz - 1 && !g.zhi_ghost) ? -g.sz : g.sz;
-    const T gz = cf[(L::NA + 2) * N + p];
-    s += (az + gz) * u[p + dzp] + (az - gz) * u[p + dzm];
-    d += T(2) * az;
+    s += (q.az + q.gz) * nb[4] + (q.az - q.gz) * nb[5];
+    d += T(2) * q.az;
   }
   if (KIND == KFULL) {
-    constexpr int E0 = L::NA + L::NG;
-    const T exy = cf[E0 * N + p];
-    s += exy * (u[p + dxp + dyp] - u[p + dxp + dym] - u[p + dxm + dyp] + u[p + dxm + dym]);
+    s += q.exy * (nb[6] - nb[7] - nb[8] + nb[9]);
     if (DIM == 3) {
-      const T exz = cf[(E0 + 1) * N + p];
-      const T eyz = cf[(E0 + 2) * N + p];
-      s += exz * (u[p + dxp + dzp] - u[p + dxp + dzm] - u[p + dxm + dzp] + u[p + dxm + dzm]);
-      s += eyz * (u[p + dyp + dzp] - u[p + dyp + dzm] - u[p + dym + dzp] + u[p + dym + dzm]);
+      s += q.exz * (nb[10] - nb[11] - nb[12] + nb[13]);
+      s += q.eyz * (nb[14] - nb[15] - nb[16] + nb[17]);
     }
   }
   D = d;
   S = s;
+}
+
+template <int DIM, int KIND>
+struct NbCount {
+  static constexpr int N = (KIND == KFULL) ? (DIM == 3 ? 18 : 10) : (DIM == 3 ? 6 : 4);
+};
+
+// gather the neighbour values of global-memory point p (i, j, k local)
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void gather_nb(const T* __restrict__ u, const Geo& g, int i, int j,
+                                          int k, int64_t p, T* nb) {
+  const int64_t dxm = (i == 0) ? 1 : -1;
+  const int64_t dxp = (i == g.nx - 1) ? -1 : 1;
+  const int64_t dym = (j == 0) ? g.sy : -g.sy;
+  const int64_t dyp = (j == g.ny - 1) ? -g.sy : g.sy;
+  nb[0] = u[p + dxp];
+  nb[1] = u[p + dxm];
+  nb[2] = u[p + dyp];
+  nb[3] = u[p + dym];
+  int64_t dzm = 0, dzp = 0;
+  if (DIM == 3) {
+    dzm = (k == 0 && !g.zlo_ghost) ? g.sz : -g.sz;
+    dzp = (k == g.nz - 1 && !g.zhi_ghost) ? -g.sz : g.sz;
+    nb[4] = u[p + dzp];
+    nb[5] = u[p + dzm];
+  }
+  if (KIND == KFULL) {
+    nb[6] = u[p + dxp + dyp];
+    nb[7] = u[p + dxp + dym];
+    nb[8] = u[p + dxm + dyp];
+    nb[9] = u[p + dxm + dym];
+    if (DIM == 3) {
+      nb[10] = u[p + dxp + dzp];
+      nb[11] = u[p + dxp + dzm];
+      nb[12] = u[p + dxm + dzp];
+      nb[13] = u[p + dxm + dzm];
+      nb[14] = u[p + dyp + dzp];
+      nb[15] = u[p + dyp + dzm];
+      nb[16] = u[p + dym + dzp];
+      nb[17] = u[p + dym + dzm];
+    }
+  }
+}
+
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* __restrict__ cf,
+                                              const Geo& g, const Rat<T>& rat, int i, int j,
+                                              int k, int64_t p, T& D, T& S) {
+  Coefs<T> q;
+  load_coefs<T, DIM, KIND>(cf, g.N, cidx(g, i, j, k), rat, q);
+  T nb[18];
+  gather_nb<T, DIM, KIND>(u, g, i, j, k, p, nb);
+  stencil_combine<T, DIM, KIND>(q, nb, D, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -156,6 +214,257 @@ __global__ void __launch_bounds__(256) gs_lex_plane_k(T* __restrict__ u, const T
   T D, S;
   stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
   u[p] = (b[p] + S) / D;
+}
+
+// ---------------------------------------------------------------------------
+// Fused multicolour GS sweep (3D): the whole sweep in ONE launch, out of place
+// (uin -> uout), bit-identical to NC in-place gs_color_k passes.
+//
+// Wavefront: at z-step k, stage c updates colour c on plane k-c.  Colour c needs
+// colours < c already updated on planes k-c-1..k-c+1 (done in earlier stages of
+// this and the previous steps) and colours > c still old (their stages run later),
+// so the stage order reproduces the colour-by-colour sweep exactly.
+// Tiles: each workgroup owns a TX x TY column of one z-chunk; stage c also
+// updates an (NC-1-c)-wide halo redundantly so no workgroup ever needs another
+// one's updated values (overlapped tiling); only the tile interior is stored.
+// LDS: ring of NC+2 planes of u over the tile + NC halo, rows stored x-parity
+// split (even x, then odd x) so every colour stage reads contiguous runs.
+// Registers: the next step's u plane and each stage's coefficients / rhs are
+// prefetched one step ahead, so HBM latency hides behind the current step.
+// z-chunks start NC-1 planes early and run NC-1 planes late (redundant), and read
+// up to NC planes beyond the chunk: on a rank slab those are the GHOST planes.
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void coefs_from_raw(const T* raw, const Rat<T>& rat, Coefs<T>& q) {
+  using L = CoefLayout<DIM, KIND>;
+  if (KIND == KISO) {
+    const T a = raw[0];
+    q.ax = a;
+    q.ay = a * rat.r[1];
+    q.az = (DIM == 3) ? a * rat.r[2] : T(0);
+  } else {
+    q.ax = raw[0];
+    q.ay = raw[1];
+    q.az = (DIM == 3) ? raw[2] : T(0);
+  }
+  q.gx = raw[L::NA];
+  q.gy = raw[L::NA + 1];
+  q.gz = (DIM == 3) ? raw[L::NA + 2] : T(0);
+  if (KIND == KFULL) {
+    q.exy = raw[L::NA + L::NG];
+    q.exz = (DIM == 3) ? raw[L::NA + L::NG + 1] : T(0);
+    q.eyz = (DIM == 3) ? raw[L::NA + L::NG + 2] : T(0);
+  } else {
+    q.exy = q.exz = q.eyz = T(0);
+  }
+}
+
+template <int NC, int TX, int TY>
+struct FusedGeom {
+  static constexpr int H = NC;
+  static constexpr int RX = TX + 2 * H;
+  static constexpr int RY = TY + 2 * H;
+  // LDS row: even-x half, then odd-x half starting HALF floats later; HALF is
+  // padded to 16 (mod 32) so lanes alternating halves hit disjoint banks.
+  static constexpr int HALF = ((RX / 2 + 15) / 32) * 32 + 16;
+  static constexpr int PITCH = 2 * HALF + 1;
+  static constexpr int PLANE = RY * PITCH;
+  static constexpr int NP = NC + 2;
+  static constexpr int rows(int c) { return (NC == 4) ? (TY + 2 * (NC - 1 - c)) / 2 : TY + 2 * (NC - 1 - c); }
+  static constexpr int cols(int c) { return (TX + 2 * (NC - 1 - c)) / 2; }
+};
+
+template <typename T, int KIND, int TX, int TY, int NT, int MINW>
+__global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin, T* __restrict__ uout,
+                                                       const T* __restrict__ b, const T* __restrict__ cf,
+                                                       Geo g, Rat<T> rat, int zc, int ntx, int nty) {
+  constexpr int NC = (KIND == KFULL) ? 4 : 2;
+  using FG = FusedGeom<NC, TX, TY>;
+  constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
+  constexpr int PLANE = FG::PLANE, NP = FG::NP;
+  constexpr int UPT = (RX * RY + NT - 1) / NT;
+  constexpr int OPT = (TX * TY + NT - 1) / NT;
+  constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr int NNB = NbCount<3, KIND>::N;
+  static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
+  static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
+  __shared__ T lds[NP * PLANE];
+
+  // XCD-aware, bijective block -> (chunk, tile): the tiles of one chunk share an XCD (L2)
+  int bid = blockIdx.x;
+  {
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = bid & 7, idx = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int tiles = ntx * nty;
+  const int chunk = bid / tiles;
+  const int tile = bid - chunk * tiles;
+  const int tyi = tile / ntx;
+  const int txi = tile - tyi * ntx;
+  const int rx0 = txi * TX - H;
+  const int ry0 = tyi * TY - H;
+  const int tid = threadIdx.x;
+  const int nx = g.nx, ny = g.ny, sy = (int)g.sy;
+  const int64_t sz = g.sz, NF = g.N;
+
+  const int zlo = g.zlo_ghost ? -GHOST : 0;          // loadable planes [zlo, zhi)
+  const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;
+  const int ulo = g.zlo_ghost ? -(GHOST - 1) : 0;    // updatable planes [ulo, uhi)
+  const int uhi = g.zhi_ghost ? g.nz + GHOST - 1 : g.nz;
+  const int z0 = chunk * zc;
+  const int z1 = min(z0 + zc, g.nz);
+  const int kbeg = z0 - (NC - 1);
+  const int kend = z1 + NC - 2;
+
+  // ---- per-thread constants (hoisted out of the z loop)
+  // region plane elements handled by this thread for loads: LDS index + in-plane offset
+  int u_lds[UPT], u_off[UPT];
+#pragma unroll
+  for (int e = 0; e < UPT; ++e) {
+    const int q = tid + e * NT;
+    const int lj = q / RX, li = q - (q / RX) * RX;
+    const int gi = rx0 + li, gj = ry0 + lj;
+    const bool ok = q < RX * RY && gi >= 0 && gi < nx && gj >= 0 && gj < ny;
+    u_lds[e] = ok ? lj * PITCH + (li & 1) * HALF + (li >> 1) : -1;
+    u_off[e] = gj * sy + gi;
+  }
+  // stage point (r, t) of this thread, per stage
+  int st_r[NC], st_t[NC];
+  bool st_has[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int cols = FG::cols(c);
+    st_has[c] = tid < FG::rows(c) * cols;
+    st_r[c] = tid / cols;
+    st_t[c] = tid - (tid / cols) * cols;
+  }
+  auto slot = [](int m) { return (m + NP * 64) % NP; };
+  auto plane_ok = [&](int m) { return m >= zlo && m < zhi; };
+  auto stage_on = [&](int c, int m) {
+    const int h = NC - 1 - c;
+    return m >= z0 - h && m < z1 + h && m >= ulo && m < uhi;
+  };
+  // (li, lj) of this thread's stage-c point on plane m
+  auto locate = [&](int c, int m, int& li, int& lj) -> bool {
+    const int h = NC - 1 - c;
+    const int l0 = H - h;
+    const int pm = (m + g.zoff) & 1;
+    if (NC == 4) {
+      lj = l0 + ((((c >> 1) ^ pm ^ l0) & 1)) + 2 * st_r[c];
+      li = l0 + (((c & 1) ^ pm ^ l0) & 1) + 2 * st_t[c];
+    } else {
+      lj = l0 + st_r[c];
+      li = l0 + ((c ^ pm ^ lj ^ l0) & 1) + 2 * st_t[c];
+    }
+    const int gi = rx0 + li, gj = ry0 + lj;
+    return st_has[c] && gi >= 0 && gi < nx && gj >= 0 && gj < ny;
+  };
+
+  T up[UPT];
+  T raw[NC][NCF];
+  T bv[NC];
+  auto load_plane = [&](int m) {
+    const T* base = uin + (int64_t)m * sz;
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) up[e] = (u_lds[e] >= 0) ? base[u_off[e]] : T(0);
+  };
+  auto put_plane = [&](int m) {
+    T* P = lds + slot(m) * PLANE;
+#pragma unroll
+    for (int e = 0; e < UPT; ++e)
+      if (u_lds[e] >= 0) P[u_lds[e]] = up[e];
+  };
+  auto load_stage = [&](int c, int k) {
+    const int m = k - c;
+    int li, lj;
+    if (stage_on(c, m) && locate(c, m, li, lj)) {
+      const int gi = rx0 + li, gj = ry0 + lj;
+      const T* cp = cf + (int64_t)m * sz;
+      const int co = gj * sy + ((gi & 1) ? g.hx0 + (gi >> 1) : (gi >> 1));
+#pragma unroll
+      for (int a = 0; a < NCF; ++a) raw[c][a] = cp[a * NF + co];
+      bv[c] = b[(int64_t)m * sz + gj * sy + gi];
+    }
+  };
+
+  // prologue: planes kbeg-1, kbeg into LDS; plane kbeg+1 and step kbeg's stage data
+  for (int m = kbeg - 1; m <= kbeg; ++m)
+    if (plane_ok(m)) {
+      load_plane(m);
+      put_plane(m);
+    }
+  if (plane_ok(kbeg + 1)) load_plane(kbeg + 1);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) load_stage(c, kbeg);
+
+  for (int k = kbeg; k <= kend; ++k) {
+    if (plane_ok(k + 1)) put_plane(k + 1);
+    if (k + 1 <= kend && plane_ok(k + 2)) load_plane(k + 2);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int m = k - c;
+      int li, lj;
+      if (stage_on(c, m) && locate(c, m, li, lj)) {
+        const int gi = rx0 + li, gj = ry0 + lj;
+        const int zm = (m == 0 && !g.zlo_ghost) ? 1 : m - 1;
+        const int zp = (m == g.nz - 1 && !g.zhi_ghost) ? g.nz - 2 : m + 1;
+        T* P0 = lds + slot(m) * PLANE;
+        const T* Pm = lds + slot(zm) * PLANE;
+        const T* Pp = lds + slot(zp) * PLANE;
+        const int il = lj * PITCH + (li & 1) * HALF + (li >> 1);
+        // split-row offsets of li +- 1 (the other parity half), mirrored at the border
+        const int ox_p = (li & 1) ? 1 - HALF : HALF;
+        const int ox_m = (li & 1) ? -HALF : HALF - 1;
+        const int oxp = (gi == nx - 1) ? ox_m : ox_p;
+        const int oxm = (gi == 0) ? ox_p : ox_m;
+        const int oyp = (gj == ny - 1) ? -PITCH : PITCH;
+        const int oym = (gj == 0) ? PITCH : -PITCH;
+        T nb[18];
+        nb[0] = P0[il + oxp];
+        nb[1] = P0[il + oxm];
+        nb[2] = P0[il + oyp];
+        nb[3] = P0[il + oym];
+        nb[4] = Pp[il];
+        nb[5] = Pm[il];
+        if (NNB == 18) {
+          nb[6] = P0[il + oxp + oyp];
+          nb[7] = P0[il + oxp + oym];
+          nb[8] = P0[il + oxm + oyp];
+          nb[9] = P0[il + oxm + oym];
+          nb[10] = Pp[il + oxp];
+          nb[11] = Pm[il + oxp];
+          nb[12] = Pp[il + oxm];
+          nb[13] = Pm[il + oxm];
+          nb[14] = Pp[il + oyp];
+          nb[15] = Pm[il + oyp];
+          nb[16] = Pp[il + oym];
+          nb[17] = Pm[il + oym];
+        }
+        Coefs<T> q;
+        coefs_from_raw<T, 3, KIND>(raw[c], rat, q);
+        const T bc = bv[c];
+        T D, S;
+        stencil_combine<T, 3, KIND>(q, nb, D, S);
+        P0[il] = (bc + S) / D;
+      }
+      // this stage's registers are free: prefetch its data for the next step
+      if (k + 1 <= kend) load_stage(c, k + 1);
+      __syncthreads();
+    }
+    // plane k-NC+1 is final on the tile: store it (coalesced rows)
+    const int mo = k - NC + 1;
+    if (mo >= z0 && mo < z1) {
+      const T* P = lds + slot(mo) * PLANE;
+      T* out = uout + (int64_t)mo * sz;
+#pragma unroll
+      for (int e = 0; e < OPT; ++e) {
+        const int q = tid + e * NT;
+        const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
+        const int gi = rx0 + li, gj = ry0 + lj;
+        if (q < TX * TY && gi < nx && gj < ny) out[gj * sy + gi] = P[lj * PITCH + (li & 1) * HALF + (li >> 1)];
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -501,26 +810,28 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
   if (i >= nx || j >= ny) return;
   const int64_t n = (int64_t)nx * ny * nz;
   const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
+  // output index in the x-parity-split coefficient layout
+  const int64_t o = (int64_t)nx * (j + (int64_t)ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1));
   const double h[3] = {hx, hy, hz};
   const int nn[3] = {nx, ny, nz};
   const int id[3] = {i, j, k};
   const int64_t st[3] = {1, nx, (int64_t)nx * ny};
   if (KIND == KISO) {
-    cf[p] = (T)(dt * M[p] / (h[0] * h[0]));
+    cf[o] = (T)(dt * M[p] / (h[0] * h[0]));
   } else {
-    for (int d = 0; d < DIM; ++d) cf[d * n + p] = (T)(dt * M[tcomp(DIM, d, d) * n + p] / (h[d] * h[d]));
+    for (int d = 0; d < DIM; ++d) cf[d * n + o] = (T)(dt * M[tcomp(DIM, d, d) * n + p] / (h[d] * h[d]));
   }
   for (int d = 0; d < DIM; ++d) {
     double s = 0.0;
     for (int d2 = 0; d2 < DIM; ++d2)
       s += delta_f(M + tcomp(DIM, d, d2) * n, p, id[d2], nn[d2], st[d2]) / (2.0 * h[d2]);
-    cf[(L::NA + d) * n + p] = (T)(dt / (2.0 * h[d]) * s);
+    cf[(L::NA + d) * n + o] = (T)(dt / (2.0 * h[d]) * s);
   }
   if (KIND == KFULL) {
     int e = L::NA + L::NG;
     for (int d = 0; d < DIM; ++d)
       for (int d2 = d + 1; d2 < DIM; ++d2, ++e)
-        cf[e * n + p] = (T)(dt * M[tcomp(DIM, d, d2) * n + p] / (2.0 * h[d] * h[d2]));
+        cf[e * n + o] = (T)(dt * M[tcomp(DIM, d, d2) * n + p] / (2.0 * h[d] * h[d2]));
   }
 }
 

@@ -268,11 +268,12 @@ class Solver final : public SolverBase {
       L.g.sy = G.n[0];
       L.g.sz = G.n[0] * G.n[1];
       L.g.N = L.g.sz * L.g.nz;
+      L.g.hx0 = (L.g.nx + 1) / 2;
       for (int d = 0; d < 3; ++d) L.cent[d] = G.cent[d];
       L.rat.r[0] = T(1);
       L.rat.r[1] = (T)((G.h[0] * G.h[0]) / (G.h[1] * G.h[1]));
       L.rat.r[2] = (T)((G.h[0] * G.h[0]) / (G.h[2] * G.h[2]));
-      L.ghost = (dim == 3) ? L.g.sz : 0;
+      L.ghost = (dim == 3) ? (int64_t)GHOST * L.g.sz : 0;
       const int64_t tot = L.g.N + 2 * L.ghost;
       for (int a = 0; a < 4; ++a) {
         HIP_CHECK(hipMalloc(&L.alloc[a], sizeof(T) * tot));
@@ -338,12 +339,49 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipGetLastError());
   }
 
-  // halo exchange of one array's boundary planes (multi-GPU; no-op on one rank)
-  void halo(int l, T* a) {
+  // halo exchange of `depth` boundary planes of one array (multi-GPU; no-op on one rank)
+  void halo(int l, T* a, int depth = 1) {
     if (!c_->comm.active() || !c_->geom[l].distributed) return;
     LevelData<T>& L = lv_[l];
-    c_->comm.exchange_planes(a, L.g.sz, L.g.nz, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
+    c_->comm.exchange_planes(a, L.g.sz, L.g.nz, depth, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
                              std::is_same<T, double>::value, c_->stream);
+  }
+
+  bool use_fused(int l) const {
+    const int v = c_->d.gs_kernel;  // 0 auto, 1 per-colour passes, 2 fused
+    if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL) return false;
+    if (v == 1) return false;
+    (void)l;
+    return true;
+  }
+
+  // one fused GS sweep x -> t, then swap (gs_fused_k)
+  float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+    LevelData<T>& L = lv_[l];
+    halo(l, L.x, GHOST);
+    constexpr int TX = 64, TY = 16;
+    const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
+    const int tiles = ntx * nty;
+    int chunks = (2048 + tiles - 1) / tiles;
+    chunks = std::max(1, std::min(chunks, std::max(1, L.g.nz / 32)));
+    const int zc = (L.g.nz + chunks - 1) / chunks;
+    chunks = (L.g.nz + zc - 1) / zc;
+    const unsigned nb = (unsigned)(tiles * chunks);
+    if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
+    if (c_->kind == KFULL)
+      hipLaunchKernelGGL((gs_fused_k<T, KFULL, TX, TY, 512, 4>), dim3(nb), dim3(512), 0, c_->stream,
+                         L.x, L.t, L.b, L.cf, L.g, L.rat, zc, ntx, nty);
+    else if (c_->kind == KDIAG)
+      hipLaunchKernelGGL((gs_fused_k<T, KDIAG, TX, TY, 1024, 4>), dim3(nb), dim3(1024), 0, c_->stream,
+                         L.x, L.t, L.b, L.cf, L.g, L.rat, zc, ntx, nty);
+    else
+      hipLaunchKernelGGL((gs_fused_k<T, KISO, TX, TY, 1024, 4>), dim3(nb), dim3(1024), 0, c_->stream,
+                         L.x, L.t, L.b, L.cf, L.g, L.rat, zc, ntx, nty);
+    if (e1) HIP_CHECK(hipEventRecord(e1, c_->stream));
+    HIP_CHECK(hipGetLastError());
+    std::swap(L.x, L.t);
+    std::swap(L.alloc[0], L.alloc[3]);
+    return 0.f;
   }
 
   void smooth(int l, unsigned n) override {
@@ -373,6 +411,8 @@ class Solver final : public SolverBase {
           });
         }
         HIP_CHECK(hipGetLastError());
+      } else if (use_fused(l)) {
+        fused_sweep(l);
       } else {
         const int nc = c_->ncolors;
         const int rows = (nc == 4) ? (L.g.ny + 1) / 2 : L.g.ny;
@@ -675,7 +715,8 @@ class Solver final : public SolverBase {
                     unsigned* launches) override {
     LevelData<T>& L = lv_[l];
     const int sm = c_->d.smoother;
-    const int nc = (sm == MAD_GAUSS_SEIDEL) ? c_->ncolors : 1;
+    const bool fused = use_fused(l);
+    const int nc = (sm == MAD_GAUSS_SEIDEL && !fused) ? c_->ncolors : 1;
     REQUIRE(sm != MAD_GAUSS_SEIDEL_LEX, MAD_ERR_UNSUPPORTED, "bench of the lexicographic mode");
     const unsigned nl = n * nc;
     std::vector<hipEvent_t> ev(2 * nl);
@@ -699,6 +740,9 @@ class Solver final : public SolverBase {
         ++q;
         std::swap(L.x, L.t);
         std::swap(L.alloc[0], L.alloc[3]);
+      } else if (fused) {
+        fused_sweep(l, ev[2 * q], ev[2 * q + 1]);
+        ++q;
       } else {
         dim3 gr = grid_for((L.g.nx + 1) / 2, rows, L.g.nz, BLK);
         for (int col = 0; col < nc; ++col) {
@@ -940,15 +984,17 @@ class Solver final : public SolverBase {
       for (int64_t j = 0; j < ny; ++j)
         for (int64_t i = 0; i < nx; ++i) {
           const int64_t p = i + nx * (j + ny * k);
+          // coefficient fields are x-parity split (mad_kernels.hpp, cidx)
+          const int64_t c = nx * (j + ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1));
           double a[3], g[3], e[3] = {0, 0, 0};
           if (kind == KISO) {
-            a[0] = cf[p]; a[1] = cf[p] * r1; a[2] = cf[p] * r2;
+            a[0] = cf[c]; a[1] = cf[c] * r1; a[2] = cf[c] * r2;
           } else {
-            for (int d = 0; d < dim; ++d) a[d] = cf[d * n + p];
+            for (int d = 0; d < dim; ++d) a[d] = cf[d * n + c];
           }
-          for (int d = 0; d < dim; ++d) g[d] = cf[(na + d) * n + p];
+          for (int d = 0; d < dim; ++d) g[d] = cf[(na + d) * n + c];
           if (kind == KFULL)
-            for (int q = 0; q < dim * (dim - 1) / 2; ++q) e[q] = cf[(na + dim + q) * n + p];
+            for (int q = 0; q < dim * (dim - 1) / 2; ++q) e[q] = cf[(na + dim + q) * n + c];
           const int64_t xm = (i == 0) ? 1 : i - 1, xp = (i == nx - 1) ? nx - 2 : i + 1;
           const int64_t ym = (j == 0) ? 1 : j - 1, yp = (j == ny - 1) ? ny - 2 : j + 1;
           const int64_t zm = (k == 0) ? 1 : k - 1, zp = (k == nz - 1) ? nz - 2 : k + 1;

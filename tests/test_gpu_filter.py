@@ -159,13 +159,14 @@ def test_vcycle_convergence_factor_at_scale(M):
         s.synth_tensor(kind=0, seed=4)
         s.setup()
         s.synth_level(0, M.capi.B, 3)
-        s.synth_level(0, M.capi.X, 3)
+        s.synth_level(0, M.capi.X, 7)  # independent initial guess: O(1) initial residual
         bn = s.norm(0, M.capi.B)
-        rel = []
+        rel = [s.residual(0) / bn]
         for _ in range(4):
             s.vcycle()
             rel.append(s.residual(0) / bn)
         res[prec] = rel
-        factors = [b / a for a, b in zip(rel, rel[1:])]
-        assert max(factors) < 0.35, rel
+        # above the fp32 rounding floor (~1e-7) every cycle reduces by a mesh-independent factor
+        factors = [b / a for a, b in zip(rel, rel[1:]) if b > 1e-6]
+        assert factors and max(factors) < 0.2, rel
     assert abs(res[M.FP32][2] - res[M.FP64][2]) < 0.05 * res[M.FP64][2]
