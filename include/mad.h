@@ -212,6 +212,11 @@ int mad_bench_synth_level(mad_ctx *ctx, int32_t level, int32_t which, uint64_t s
  * The unique id (128 bytes) is created on rank 0 and broadcast by the host. */
 int mad_comm_unique_id(void *uid128);
 int mad_comm_init(mad_ctx *ctx, const void *uid128);
+/* In-process transport: the contexts of one process that pass the same `group`
+ * (each with its own desc.rank, driven from its own host thread) exchange
+ * ghost planes by device-to-device copies.  Same bytes as the RCCL path; used to
+ * test the z-slab decomposition on a single GPU. */
+int mad_comm_init_local(mad_ctx *ctx, uint64_t group);
 /* slab [z_begin, z_end) of this rank for a global nz (even-aligned split) */
 int mad_slab_range(int64_t nz, int32_t nranks, int32_t rank, int32_t align, int64_t *z_begin,
                    int64_t *z_end);

@@ -36,7 +36,8 @@ EXPORTS = (
     "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
     "mad_interpolate", "mad_prolongate_add", "mad_coarse_solve", "mad_vcycle", "mad_fmg",
     "mad_synchronize", "mad_bench_smooth", "mad_bench_vcycle", "mad_bench_synth_tensor",
-    "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_slab_range",
+    "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_comm_init_local",
+    "mad_slab_range",
 )
 
 
@@ -145,6 +146,7 @@ def load():
         "mad_bench_synth_level": ([vp, i32, i32, ctypes.c_uint64], i32),
         "mad_comm_unique_id": ([vp], i32),
         "mad_comm_init": ([vp, vp], i32),
+        "mad_comm_init_local": ([vp, ctypes.c_uint64], i32),
         "mad_slab_range": ([i64, i32, i32, i32, i64p, i64p], i32),
     }
     for name, (args, res) in sig.items():

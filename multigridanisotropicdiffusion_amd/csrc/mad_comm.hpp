@@ -1,19 +1,32 @@
-// mad_comm.hpp -- RCCL transport for the z-slab decomposition (one process per
-// GPU, collectives over xGMI).  The reference is single-threaded and has no
-// distributed path; this is the MI355X addition.
+// mad_comm.hpp -- transports for the z-slab decomposition.
 //
-// Exchanges used by the solver:
-//   exchange_planes   one ghost plane per z face with rank +-1 (grouped send/recv)
+// The reference is single-threaded and has no distributed path; this is the
+// MI355X addition.  Two interchangeable backends implement the
+// three exchanges the solver uses:
+//   exchange_planes   `depth` ghost planes per z face with rank +-1
 //   allreduce_sum_f64 ||r||^2 partial sums (8 bytes per V-cycle)
 //   allgather_slabs   hand-over from the deepest distributed level to the first
-//                     replicated coarse level (<= a few hundred KiB)
+//                     replicated coarse level (a few hundred KiB)
+// RCCL   one process per GPU, grouped ncclSend/ncclRecv + collectives over xGMI.
+// LOCAL  several ranks as host threads of ONE process (any device, typically the
+//        same GPU): device-to-device copies between the ranks' own arrays, host
+//        barriers for ordering.  It exists so the decomposition (ghost planes,
+//        global colour parity, coarsening alignment, agglomeration) is testable
+//        bit-for-bit on a one-GPU machine; RCCL and LOCAL move the same bytes.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace mad {
 
@@ -27,8 +40,55 @@ struct CommError : std::runtime_error {
     if (r_ != ncclSuccess) throw CommError(std::string(#x) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+#define HIPC_CHECK(x)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) throw CommError(std::string(#x) + ": " + hipGetErrorString(e_));  \
+  } while (0)
+
+// process-local rendezvous for the LOCAL backend
+struct LocalGroup {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const void*> ptr;   // per-rank published array base (plane 0)
+  std::vector<double> val;        // per-rank scalars for allreduce
+  explicit LocalGroup(int nranks) : n(nranks), ptr(nranks, nullptr), val(nranks, 0.0) {}
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t gen = generation;
+    if (++arrived == n) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; })) {
+      throw CommError("local group barrier timed out (a rank failed or diverged)");
+    }
+  }
+};
+
+inline std::shared_ptr<LocalGroup> local_group(uint64_t key, int nranks) {
+  static std::mutex m;
+  static std::map<uint64_t, std::weak_ptr<LocalGroup>> groups;
+  std::lock_guard<std::mutex> lk(m);
+  auto it = groups.find(key);
+  if (it != groups.end()) {
+    if (auto g = it->second.lock()) {
+      if (g->n != nranks) throw CommError("local group size mismatch");
+      return g;
+    }
+  }
+  auto g = std::make_shared<LocalGroup>(nranks);
+  groups[key] = g;
+  return g;
+}
+
 class Comm {
  public:
+  enum Mode { NONE, RCCL, LOCAL };
+
   static void unique_id(void* out128) {
     ncclUniqueId id;
     NCCL_CHECK(ncclGetUniqueId(&id));
@@ -43,54 +103,112 @@ class Comm {
     std::memcpy(&id, uid128, sizeof(id));
     (void)device;
     NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    mode_ = RCCL;
     nranks_ = nranks;
     rank_ = rank;
+  }
+
+  void init_local(uint64_t key, int nranks, int rank) {
+    destroy();
+    if (nranks <= 1) return;
+    group_ = local_group(key, nranks);
+    mode_ = LOCAL;
+    nranks_ = nranks;
+    rank_ = rank;
+    group_->barrier();  // everyone joined
   }
 
   void destroy() {
     if (comm_) (void)ncclCommDestroy(comm_);
     comm_ = nullptr;
+    group_.reset();
+    mode_ = NONE;
     nranks_ = 1;
     rank_ = 0;
   }
 
-  bool active() const { return comm_ != nullptr && nranks_ > 1; }
+  bool active() const { return mode_ != NONE && nranks_ > 1; }
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
 
   // a: base pointer of local plane 0; planes -depth..-1 and nz..nz+depth-1 are ghosts.
-  // Sends the first / last `depth` owned planes to rank -+ 1 (one grouped call).
+  // The first / last `depth` owned planes go to rank -+ 1.
   void exchange_planes(void* a, int64_t plane, int nz, int depth, int has_lo, int has_hi,
                        size_t esz, bool is_double, hipStream_t s) {
     char* base = (char*)a;
-    const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
     const size_t pb = (size_t)plane * esz;
-    const size_t cnt = (size_t)plane * depth;
-    NCCL_CHECK(ncclGroupStart());
+    if (mode_ == RCCL) {
+      const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
+      const size_t cnt = (size_t)plane * depth;
+      NCCL_CHECK(ncclGroupStart());
+      if (has_lo) {
+        NCCL_CHECK(ncclSend(base, cnt, dt, rank_ - 1, comm_, s));
+        NCCL_CHECK(ncclRecv(base - depth * pb, cnt, dt, rank_ - 1, comm_, s));
+      }
+      if (has_hi) {
+        NCCL_CHECK(ncclSend(base + (size_t)(nz - depth) * pb, cnt, dt, rank_ + 1, comm_, s));
+        NCCL_CHECK(ncclRecv(base + (size_t)nz * pb, cnt, dt, rank_ + 1, comm_, s));
+      }
+      NCCL_CHECK(ncclGroupEnd());
+      return;
+    }
+    // LOCAL: publish, pull the neighbours' boundary planes, wait until all pulled
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->ptr[rank_] = a;
+    group_->barrier();
     if (has_lo) {
-      NCCL_CHECK(ncclSend(base, cnt, dt, rank_ - 1, comm_, s));
-      NCCL_CHECK(ncclRecv(base - depth * pb, cnt, dt, rank_ - 1, comm_, s));
+      const char* nb = (const char*)group_->ptr[rank_ - 1];  // same nz on every rank
+      HIPC_CHECK(hipMemcpyAsync(base - depth * pb, nb + (size_t)(nz - depth) * pb, depth * pb,
+                                hipMemcpyDeviceToDevice, s));
     }
     if (has_hi) {
-      NCCL_CHECK(ncclSend(base + (size_t)(nz - depth) * pb, cnt, dt, rank_ + 1, comm_, s));
-      NCCL_CHECK(ncclRecv(base + (size_t)nz * pb, cnt, dt, rank_ + 1, comm_, s));
+      const char* nb = (const char*)group_->ptr[rank_ + 1];
+      HIPC_CHECK(hipMemcpyAsync(base + (size_t)nz * pb, nb, depth * pb, hipMemcpyDeviceToDevice, s));
     }
-    NCCL_CHECK(ncclGroupEnd());
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->barrier();
   }
 
   void allreduce_sum_f64(double* p, size_t n, hipStream_t s) {
-    NCCL_CHECK(ncclAllReduce(p, p, n, ncclDouble, ncclSum, comm_, s));
+    if (mode_ == RCCL) {
+      NCCL_CHECK(ncclAllReduce(p, p, n, ncclDouble, ncclSum, comm_, s));
+      return;
+    }
+    if (n != 1) throw CommError("local allreduce supports one value");
+    double v = 0.0;
+    HIPC_CHECK(hipMemcpyAsync(&v, p, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->val[rank_] = v;
+    group_->barrier();
+    double sum = 0.0;
+    for (int r = 0; r < nranks_; ++r) sum += group_->val[r];  // rank order: deterministic
+    group_->barrier();
+    HIPC_CHECK(hipMemcpyAsync(p, &sum, sizeof(double), hipMemcpyHostToDevice, s));
+    HIPC_CHECK(hipStreamSynchronize(s));
   }
 
   // every rank holds nz_global / nranks planes; gather all slabs in rank order
   void allgather_slabs(const void* slab, void* full, int64_t plane, int64_t nz_global, size_t esz,
                        hipStream_t s) {
-    const size_t count = (size_t)plane * (size_t)(nz_global / nranks_) * (esz / 4);
-    NCCL_CHECK(ncclAllGather(slab, full, count, ncclFloat, comm_, s));
+    const size_t bytes = (size_t)plane * (size_t)(nz_global / nranks_) * esz;
+    if (mode_ == RCCL) {
+      NCCL_CHECK(ncclAllGather(slab, full, bytes / 4, ncclFloat, comm_, s));
+      return;
+    }
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->ptr[rank_] = slab;
+    group_->barrier();
+    for (int r = 0; r < nranks_; ++r)
+      HIPC_CHECK(hipMemcpyAsync((char*)full + r * bytes, group_->ptr[r], bytes,
+                                hipMemcpyDeviceToDevice, s));
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->barrier();
   }
 
  private:
+  Mode mode_ = NONE;
   ncclComm_t comm_ = nullptr;
+  std::shared_ptr<LocalGroup> group_;
   int nranks_ = 1;
   int rank_ = 0;
 };

@@ -52,7 +52,8 @@ struct Geo {
   int zhi_ghost;        // 1: planes nz..nz+GHOST-1 hold the upper neighbour's data
   int hx0;              // (nx + 1) / 2: start of the odd-x half of a coefficient row
   int64_t sy, sz;       // strides
-  int64_t N;            // nx*ny*nz (coefficient field stride)
+  int64_t N;            // nx*ny*nz (owned points)
+  int64_t cs;           // coefficient field stride (N, + 2*GHOST planes on rank slabs)
 };
 
 __device__ __forceinline__ int64_t cidx(const Geo& g, int i, int j, int k) {
@@ -157,7 +158,7 @@ __device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* 
                                               const Geo& g, const Rat<T>& rat, int i, int j,
                                               int k, int64_t p, T& D, T& S) {
   Coefs<T> q;
-  load_coefs<T, DIM, KIND>(cf, g.N, cidx(g, i, j, k), rat, q);
+  load_coefs<T, DIM, KIND>(cf, g.cs, cidx(g, i, j, k), rat, q);
   T nb[18];
   gather_nb<T, DIM, KIND>(u, g, i, j, k, p, nb);
   stencil_combine<T, DIM, KIND>(q, nb, D, S);
@@ -304,7 +305,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
   const int ry0 = tyi * TY - H;
   const int tid = threadIdx.x;
   const int nx = g.nx, ny = g.ny, sy = (int)g.sy;
-  const int64_t sz = g.sz, NF = g.N;
+  const int64_t sz = g.sz, NF = g.cs;
 
   const int zlo = g.zlo_ghost ? -GHOST : 0;          // loadable planes [zlo, zhi)
   const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;

@@ -238,9 +238,11 @@ struct LevelData {
   T* b = nullptr;  // rhs
   T* r = nullptr;  // residual
   T* t = nullptr;  // WJ ping-pong / scratch
-  T* cf = nullptr;
+  T* cf = nullptr;        // field 0, plane 0 (ghost planes precede it on rank slabs)
+  T* cf_alloc = nullptr;
   Rat<T> rat{};
-  int64_t ghost = 0;  // elements of one ghost plane (3D: sz)
+  int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
+  bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
 };
 
 template <typename T>
@@ -283,7 +285,13 @@ class Solver final : public SolverBase {
       L.b = L.alloc[1] + L.ghost;
       L.r = L.alloc[2] + L.ghost;
       L.t = L.alloc[3] + L.ghost;
-      HIP_CHECK(hipMalloc(&L.cf, sizeof(T) * L.g.N * ncoef_));
+      // coefficient fields: rank slabs keep GHOST planes per side (the fused sweep
+      // recomputes colours on the ghost planes, csrc/mad_kernels.hpp gs_fused_k)
+      const int64_t cg = G.distributed ? (int64_t)GHOST * L.g.sz : 0;
+      L.g.cs = L.g.N + 2 * cg;
+      HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * L.g.cs * ncoef_));
+      HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * L.g.cs * ncoef_, c->stream));
+      L.cf = L.cf_alloc + cg;
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
@@ -306,6 +314,7 @@ class Solver final : public SolverBase {
 
   void upload(int l, int which, const double* h) override {
     LevelData<T>& L = lv_[l];
+    if (which == MAD_B) L.b_halo_ok = false;
     double* tmp = scratch64(L.g.N);
     HIP_CHECK(hipMemcpyAsync(tmp, h, sizeof(double) * L.g.N, hipMemcpyHostToDevice, c_->stream));
     hipLaunchKernelGGL((convert_k<double, T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream,
@@ -326,6 +335,7 @@ class Solver final : public SolverBase {
 
   void fill(int l, int which, double v) override {
     LevelData<T>& L = lv_[l];
+    if (which == MAD_B) L.b_halo_ok = false;
     hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, arr(l, which),
                        L.g.N, (T)v);
     HIP_CHECK(hipGetLastError());
@@ -333,6 +343,7 @@ class Solver final : public SolverBase {
 
   void synth_level(int l, int which, uint64_t seed) override {
     LevelData<T>& L = lv_[l];
+    if (which == MAD_B) L.b_halo_ok = false;
     const LevelGeom& G = c_->geom[l];
     hipLaunchKernelGGL((synth_image_k<T>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK), BLK, 0, c_->stream,
                        arr(l, which), L.g, G.n[0], G.n[1], seed);
@@ -359,6 +370,10 @@ class Solver final : public SolverBase {
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
+    if (!L.b_halo_ok) {
+      halo(l, L.b, GHOST);
+      L.b_halo_ok = true;
+    }
     constexpr int TX = 64, TY = 16;
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
@@ -465,6 +480,7 @@ class Solver final : public SolverBase {
   void restrict_arr(int l, T* fine, T* coarse) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
+    C.b_halo_ok = false;
     REQUIRE(!c_->geom[l].distributed || c_->geom[l + 1].distributed, MAD_ERR_UNSUPPORTED,
             "restriction onto a replicated level");
     halo(l, fine);
@@ -628,6 +644,7 @@ class Solver final : public SolverBase {
       src = stage;
     }
     convert_in(src, in_dtype, L0.b, N);
+    L0.b_halo_ok = false;
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
@@ -681,6 +698,7 @@ class Solver final : public SolverBase {
       c_->step_relres.push_back(relres);
       HIP_CHECK(hipMemcpyAsync(L0.b, L0.x, sizeof(T) * N, hipMemcpyDeviceToDevice,
                                c_->stream));  // MAD.hxx:248-261
+      L0.b_halo_ok = false;
     }
     HIP_CHECK(hipEventRecord(e1, c_->stream));
     // cast solution -> output type (MAD.hxx:266-289)
@@ -810,7 +828,7 @@ class Solver final : public SolverBase {
     for (auto& L : lv_) {
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
-      if (L.cf) (void)hipFree(L.cf);
+      if (L.cf_alloc) (void)hipFree(L.cf_alloc);
     }
     lv_.clear();
     if (part_) (void)hipFree(part_);
@@ -927,10 +945,14 @@ class Solver final : public SolverBase {
       });
       HIP_CHECK(hipGetLastError());
       if (slab) {
+        // owned planes plus up to GHOST neighbour planes on each side
         const int64_t plane = G.n[0] * G.n[1];
+        const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
+        const int64_t p1 = std::min<int64_t>(G.z1 + GHOST, G.n[2]);
         for (int a = 0; a < ncoef_; ++a)
-          HIP_CHECK(hipMemcpyAsync(L.cf + a * L.g.N, full_cf + a * Ng + G.z0 * plane,
-                                   sizeof(T) * L.g.N, hipMemcpyDeviceToDevice, c_->stream));
+          HIP_CHECK(hipMemcpyAsync(L.cf + a * L.g.cs + (p0 - G.z0) * plane,
+                                   full_cf + a * Ng + p0 * plane, sizeof(T) * (p1 - p0) * plane,
+                                   hipMemcpyDeviceToDevice, c_->stream));
         HIP_CHECK(hipStreamSynchronize(c_->stream));
         HIP_CHECK(hipFree(full_cf));
         full_cf = nullptr;
@@ -1055,6 +1077,7 @@ class Solver final : public SolverBase {
   void restrict_full(int l, const T* fine_full, T* coarse) {
     const LevelGeom& Gf = c_->geom[l];
     LevelData<T>& C = lv_[l + 1];
+    C.b_halo_ok = false;
     Geo gf{};
     gf.nx = (int)Gf.n[0]; gf.ny = (int)Gf.n[1]; gf.nz = (int)Gf.n[2];
     gf.sy = Gf.n[0]; gf.sz = Gf.n[0] * Gf.n[1]; gf.N = Gf.N;
@@ -1543,8 +1566,18 @@ int mad_comm_unique_id(void* uid128) {
 int mad_comm_init(mad_ctx* c, const void* uid128) {
   if (!c || !uid128) return MAD_ERR_INVALID;
   return guarded(c, [&] {
+    REQUIRE(!c->setup_done, MAD_ERR_STATE, "mad_comm_init must precede mad_setup");
     use_device(c);
     c->comm.init(uid128, c->d.nranks, c->d.rank, c->device);
+  });
+}
+
+int mad_comm_init_local(mad_ctx* c, uint64_t group) {
+  if (!c) return MAD_ERR_INVALID;
+  return guarded(c, [&] {
+    REQUIRE(!c->setup_done, MAD_ERR_STATE, "mad_comm_init_local must precede mad_setup");
+    use_device(c);
+    c->comm.init_local(group, c->d.nranks, c->d.rank);
   });
 }
 

@@ -1,0 +1,86 @@
+"""z-slab multi-GPU helpers (one rank per GPU, RCCL over xGMI).
+
+The decomposition itself lives in the C++ library (plan_geometry in
+csrc/mad_solver.hip, transports in csrc/mad_comm.hpp).  This module only
+bootstraps it:
+
+* ``bootstrap_rccl(solver, dist)`` -- rank 0 creates the RCCL unique id and
+  broadcasts it over an initialised torch.distributed process group (gloo is
+  enough: 128 bytes, once), then every rank joins the communicator.
+* ``run_local(nranks, body)`` -- runs ``nranks`` ranks as host threads of this
+  process on one device with the in-process transport (tests / rehearsal).
+* ``slabs(global_shape, nranks)`` -- the level-0 slab of every rank, from the
+  host-only planner (mad_plan_level).
+"""
+import ctypes
+import threading
+import zlib
+
+from . import _capi as C
+from .solver import Solver, comm_unique_id
+
+
+def plan(global_shape, nranks=1, rank=0):
+    """Per-level plan of one rank: list of dicts(size (x,y,z), z0, z1, distributed)."""
+    d = C.default_desc()
+    dim = len(global_shape)
+    d.dim = dim
+    size = list(reversed(global_shape)) + [1] * (3 - dim)
+    for q in range(3):
+        d.size[q] = size[q]
+    d.nranks, d.rank = nranks, rank
+    L = C.load()
+    out, l, nl = [], 0, 1
+    while l < nl:
+        n = (ctypes.c_int64 * 3)()
+        z0, z1, dist = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        r = L.mad_plan_level(ctypes.byref(d), l, n, None, None, ctypes.byref(z0),
+                             ctypes.byref(z1), ctypes.byref(dist))
+        if r < 0:
+            raise C.MadError(-r, L.mad_last_error(None).decode())
+        nl = r
+        out.append(dict(size=tuple(n), z0=z0.value, z1=z1.value, distributed=bool(dist.value)))
+        l += 1
+    return out
+
+
+def slabs(global_shape, nranks):
+    return [(p[0]["z0"], p[0]["z1"]) for p in (plan(global_shape, nranks, r) for r in range(nranks))]
+
+
+def bootstrap_rccl(solver, dist):
+    """Join the RCCL communicator; `dist` is an initialised torch.distributed."""
+    import torch
+    uid = comm_unique_id() if dist.get_rank() == 0 else bytes(128)
+    t = torch.tensor(list(uid), dtype=torch.uint8)
+    dist.broadcast(t, src=0)
+    solver.comm_init(bytes(t.tolist()))
+
+
+def run_local(nranks, body, global_shape, group=None, **solver_kw):
+    """Run body(rank, solver) on `nranks` host threads sharing one process (and
+    device), each with its z-slab context joined to an in-process group.
+    Returns the list of body results (rank order); re-raises the first error."""
+    sl = slabs(global_shape, nranks)
+    key = group if group is not None else zlib.crc32(repr((global_shape, nranks)).encode())
+    results = [None] * nranks
+    errors = []
+
+    def worker(r):
+        try:
+            z0, z1 = sl[r]
+            shape = (z1 - z0,) + tuple(global_shape[1:])
+            s = Solver(shape, nranks=nranks, rank=r, global_shape=global_shape, **solver_kw)
+            s.comm_init_local(key)
+            results[r] = body(r, s)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errors.append((r, e))
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errors:
+        raise errors[0][1]
+    return results

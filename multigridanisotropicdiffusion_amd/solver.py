@@ -123,6 +123,10 @@ class Solver:
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         self._check(self._L.mad_comm_init(self._ctx, buf))
 
+    def comm_init_local(self, group):
+        """In-process transport: contexts sharing `group` exchange slabs directly."""
+        self._check(self._L.mad_comm_init_local(self._ctx, int(group)))
+
     def setup(self):
         self._check(self._L.mad_setup(self._ctx))
 

@@ -1,0 +1,186 @@
+"""z-slab decomposition on the CPU with torch.distributed gloo, world_size 2.
+
+1. Every rank plans the hierarchy through the real C ABI (mad_plan_level); the
+   ranks agree that slabs tile each distributed level and coarse levels are
+   replicated.
+2. A numpy model of the exchange protocols the HIP path implements
+   (csrc/mad_solver.hip halo(), csrc/mad_comm.hpp) reproduces the single-rank
+   4-colour Gauss-Seidel sweep bit for bit:
+     (a) per-colour passes, 1 ghost plane exchanged before every colour
+         (gs_color_k path);
+     (b) communication-avoiding: ONE exchange of GHOST = 4 planes of u_old per
+         sweep, colour c recomputed on NC-1-c ghost planes, owned planes kept
+         (gs_fused_k path).
+   Operator: the matrix-free form of tests/mf_numpy.py; colour parity uses the
+   GLOBAL z index; mirror ghosts only at the global z faces.
+"""
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+
+import mf_numpy as mf
+import synth
+
+SHAPE = (16, 10, 9)   # (z, y, x)
+GHOST = 4
+NC = 4
+
+
+def colour(k, j, i):
+    return ((i + k) & 1) | (((j + k) & 1) << 1)
+
+
+class Window:
+    """Planes [lo, hi) of a global array (global plane indexing)."""
+
+    def __init__(self, lo, hi, nz):
+        self.lo, self.hi, self.nz = lo, hi, nz
+        self.u = np.zeros((hi - lo,) + SHAPE[1:])
+
+    def get(self, k, j, i):
+        ny, nx = SHAPE[1:]
+        i = 1 if i < 0 else (nx - 2 if i > nx - 1 else i)
+        j = 1 if j < 0 else (ny - 2 if j > ny - 1 else j)
+        k = 1 if k < 0 else (self.nz - 2 if k > self.nz - 1 else k)  # global faces only
+        assert self.lo <= k < self.hi, "read outside the window"
+        return self.u[k - self.lo, j, i]
+
+
+def update(W, b, co, k, j, i):
+    """(b + S) / D at global (k, j, i) -- same expression order as stencil_combine."""
+    at = lambda dk, dj, di: W.get(k + dk, j + dj, i + di)  # noqa: E731
+    a, g, e = co["a"], co["g"], co["e"]
+    ax, ay, az = a[0][k, j, i], a[1][k, j, i], a[2][k, j, i]
+    gx, gy, gz = g[0][k, j, i], g[1][k, j, i], g[2][k, j, i]
+    s = (ax + gx) * at(0, 0, 1) + (ax - gx) * at(0, 0, -1) + (ay + gy) * at(0, 1, 0) + (ay - gy) * at(0, -1, 0)
+    s += (az + gz) * at(1, 0, 0) + (az - gz) * at(-1, 0, 0)
+    s += e[(0, 1)][k, j, i] * (at(0, 1, 1) - at(0, -1, 1) - at(0, 1, -1) + at(0, -1, -1))
+    s += e[(0, 2)][k, j, i] * (at(1, 0, 1) - at(-1, 0, 1) - at(1, 0, -1) + at(-1, 0, -1))
+    s += e[(1, 2)][k, j, i] * (at(1, 1, 0) - at(-1, 1, 0) - at(1, -1, 0) + at(-1, -1, 0))
+    d = 1.0 + 2.0 * (ax + ay) + 2.0 * az
+    return (b[k, j, i] + s) / d
+
+
+def colour_pass(W, b, co, c, k_lo, k_hi):
+    for k in range(max(k_lo, 0), min(k_hi, W.nz)):
+        for j in range(SHAPE[1]):
+            for i in range(SHAPE[2]):
+                if colour(k, j, i) == c:
+                    W.u[k - W.lo, j, i] = update(W, b, co, k, j, i)
+
+
+def _worker(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from multigridanisotropicdiffusion_amd import distributed as D
+        # 1. plan through the C ABI, gathered across ranks
+        p = D.plan((512, 512, 512), world, rank)
+        t = torch.tensor([[lv["z0"], lv["z1"], int(lv["distributed"])] for lv in p], dtype=torch.int64)
+        allp = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allp, t)
+        # 2. exchange protocols
+        nz = SHAPE[0]
+        T = synth.random_spd(SHAPE, seed=3)
+        co = mf.coefficients(T, (1.0, 1.0, 1.0), 0.6)
+        x = synth.image(SHAPE, seed=1)
+        b = synth.image(SHAPE, seed=2)
+        z0, z1 = rank * (SHAPE[0] // world), (rank + 1) * (SHAPE[0] // world)
+        lo_nb = rank - 1 if rank > 0 else None
+        hi_nb = rank + 1 if rank < world - 1 else None
+
+        def exchange(W, depth):
+            """send owned boundary planes, receive ghosts (mad_comm.hpp exchange_planes)"""
+            reqs = []
+            if lo_nb is not None:
+                reqs.append(dist.isend(torch.from_numpy(W.u[z0 - W.lo:z0 - W.lo + depth].copy()), lo_nb))
+            if hi_nb is not None:
+                reqs.append(dist.isend(torch.from_numpy(W.u[z1 - W.lo - depth:z1 - W.lo].copy()), hi_nb))
+            for nb, at in ((lo_nb, z0 - depth), (hi_nb, z1)):
+                if nb is not None:
+                    buf = torch.zeros((depth,) + SHAPE[1:], dtype=torch.float64)
+                    dist.recv(buf, nb)
+                    W.u[at - W.lo:at - W.lo + depth] = buf.numpy()
+            for r in reqs:
+                r.wait()
+
+        def window(depth):
+            lo = z0 - depth if lo_nb is not None else z0
+            hi = z1 + depth if hi_nb is not None else z1
+            W = Window(lo, hi, nz)
+            W.u[z0 - lo:z1 - lo] = x[z0:z1]
+            return W
+
+        # (a) per-colour passes with a 1-plane exchange before every colour
+        Wa = window(1)
+        for c in range(NC):
+            exchange(Wa, 1)
+            colour_pass(Wa, b, co, c, z0, z1)
+        # (b) one GHOST-deep exchange of u_old, redundant colours on the ghost planes
+        Wb = window(GHOST)
+        exchange(Wb, GHOST)
+        for c in range(NC):
+            h = NC - 1 - c
+            colour_pass(Wb, b, co, c, max(z0 - h, Wb.lo + 1 if lo_nb is not None else 0),
+                        min(z1 + h, Wb.hi - 1 if hi_nb is not None else nz))
+        res = (Wa.u[z0 - Wa.lo:z1 - Wa.lo].copy(), Wb.u[z0 - Wb.lo:z1 - Wb.lo].copy())
+        ref = None
+        if rank == 0:
+            Wr = Window(0, nz, nz)
+            Wr.u[:] = x
+            for c in range(NC):
+                colour_pass(Wr, b, co, c, 0, nz)
+            ref = Wr.u
+        q.put((rank, [a.tolist() for a in allp], res, ref, z0, z1, None))
+        dist.destroy_process_group()
+    except BaseException:  # noqa: BLE001
+        q.put((rank, None, None, None, 0, 0, traceback.format_exc()))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_slab_protocols():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r = q.get(timeout=240)
+            assert r[6] is None, r[6]
+            out[r[0]] = r
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.terminate()
+    plans = out[0][1]
+    assert plans == out[1][1]
+    for l in range(len(plans[0])):
+        flags = {plans[r][l][2] for r in range(world)}
+        assert len(flags) == 1
+        if plans[0][l][2]:
+            assert plans[0][l][0] == 0 and plans[0][l][1] == plans[1][l][0]
+    ref = out[0][3]
+    for r in range(world):
+        _, _, (ra, rb), _, z0, z1, _ = out[r]
+        np.testing.assert_array_equal(ra, ref[z0:z1])
+        np.testing.assert_array_equal(rb, ref[z0:z1])

@@ -169,4 +169,5 @@ def test_vcycle_convergence_factor_at_scale(M):
         # above the fp32 rounding floor (~1e-7) every cycle reduces by a mesh-independent factor
         factors = [b / a for a, b in zip(rel, rel[1:]) if b > 1e-6]
         assert factors and max(factors) < 0.2, rel
-    assert abs(res[M.FP32][2] - res[M.FP64][2]) < 0.05 * res[M.FP64][2]
+    # cycle 1 is well above the fp32 floor: both precisions follow the same history
+    assert abs(res[M.FP32][1] - res[M.FP64][1]) < 0.05 * res[M.FP64][1]
