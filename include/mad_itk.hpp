@@ -1,0 +1,190 @@
+// mad_itk.hpp -- header-only, ITK-shaped C++ facade over the C ABI (mad.h).
+//
+// Mirrors the reference's filter surface so call sites port verbatim:
+//   itk::MultigridAnisotropicDiffusionImageFilter<TIn, TOut, TSmoother>
+//     include/itkMultigridAnisotropicDiffusionImageFilter.h:89-160
+//   smoother plug-ins  mad::MultigridGaussSeidelSmoother<D> / MultigridWeightedJacobiSmoother<D>
+//     include/mad/itkMultigridGaussSeidelSmoother.h, itkMultigridWeightedJacobiSmoother.h
+// ITK itself is not a dependency: images are the small mad::itkshim::Image below
+// (buffer + size + spacing + origin, x fastest, region index 0).  With a real
+// ITK build the same class body sits behind itk::ImageToImageFilter: GenerateData
+// forwards GetInput()->GetBufferPointer() etc. to Run().
+#ifndef MAD_ITK_HPP
+#define MAD_ITK_HPP
+
+#include <array>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "mad.h"
+
+namespace mad {
+namespace itkshim {
+
+template <typename T>
+struct PixelTraits;
+template <> struct PixelTraits<uint8_t> { static constexpr int32_t id = MAD_U8; };
+template <> struct PixelTraits<int8_t> { static constexpr int32_t id = MAD_I8; };
+template <> struct PixelTraits<uint16_t> { static constexpr int32_t id = MAD_U16; };
+template <> struct PixelTraits<int16_t> { static constexpr int32_t id = MAD_I16; };
+template <> struct PixelTraits<uint32_t> { static constexpr int32_t id = MAD_U32; };
+template <> struct PixelTraits<int32_t> { static constexpr int32_t id = MAD_I32; };
+template <> struct PixelTraits<float> { static constexpr int32_t id = MAD_F32; };
+template <> struct PixelTraits<double> { static constexpr int32_t id = MAD_F64; };
+
+// itk::Image<TPixel, VDim> stand-in (LargestPossibleRegion with index 0)
+template <typename TPixel, unsigned int VDim>
+class Image {
+ public:
+  using PixelType = TPixel;
+  static constexpr unsigned int ImageDimension = VDim;
+  using Pointer = std::shared_ptr<Image>;
+  using SizeType = std::array<int64_t, VDim>;
+  using SpacingType = std::array<double, VDim>;
+
+  static Pointer New() { return std::make_shared<Image>(); }
+  void SetRegions(const SizeType& s) { size_ = s; }
+  void Allocate() {
+    int64_t n = 1;
+    for (auto v : size_) n *= v;
+    buf_.assign((size_t)n, TPixel());
+  }
+  void SetSpacing(const SpacingType& s) { spacing_ = s; }
+  void SetOrigin(const SpacingType& o) { origin_ = o; }
+  const SizeType& GetSize() const { return size_; }
+  const SpacingType& GetSpacing() const { return spacing_; }
+  const SpacingType& GetOrigin() const { return origin_; }
+  TPixel* GetBufferPointer() { return buf_.data(); }
+  const TPixel* GetBufferPointer() const { return buf_.data(); }
+  int64_t NumberOfPixels() const { return (int64_t)buf_.size(); }
+
+ private:
+  SizeType size_{};
+  SpacingType spacing_{};
+  SpacingType origin_{};
+  std::vector<TPixel> buf_;
+};
+
+// itk::SymmetricSecondRankTensor<T, D>: D(D+1)/2 components, ITK order
+template <typename T, unsigned int VDim>
+struct SymmetricSecondRankTensor {
+  std::array<T, VDim * (VDim + 1) / 2> c{};
+  T& operator()(unsigned r, unsigned q) {
+    if (r > q) std::swap(r, q);
+    return c[r * VDim - r * (r - 1) / 2 + (q - r)];
+  }
+};
+
+}  // namespace itkshim
+
+// smoother plug-ins (template argument TSmootherType)
+template <unsigned int VDim>
+struct MultigridGaussSeidelSmoother {
+  static constexpr int32_t id = MAD_GAUSS_SEIDEL;
+};
+template <unsigned int VDim>
+struct MultigridGaussSeidelLexSmoother {
+  static constexpr int32_t id = MAD_GAUSS_SEIDEL_LEX;
+};
+template <unsigned int VDim>
+struct MultigridWeightedJacobiSmoother {
+  static constexpr int32_t id = MAD_WEIGHTED_JACOBI;
+};
+
+class Error : public std::runtime_error {
+ public:
+  Error(int code, const std::string& m) : std::runtime_error(m), code_(code) {}
+  int code() const { return code_; }
+
+ private:
+  int code_;
+};
+
+inline void check(int rc, const mad_ctx* c = nullptr) {
+  if (rc != MAD_OK) throw Error(rc, std::string("mad: ") + mad_last_error(c));
+}
+
+template <class TInputImage, class TOutputImage,
+          class TSmootherType = MultigridGaussSeidelSmoother<TInputImage::ImageDimension>>
+class MultigridAnisotropicDiffusionImageFilter {
+ public:
+  using Self = MultigridAnisotropicDiffusionImageFilter;
+  using Pointer = std::shared_ptr<Self>;
+  using InputPixelType = typename TInputImage::PixelType;
+  using OutputPixelType = typename TOutputImage::PixelType;
+  static constexpr unsigned int Dim = TInputImage::ImageDimension;
+  using InputTensorImageType =
+      itkshim::Image<itkshim::SymmetricSecondRankTensor<InputPixelType, Dim>, Dim>;
+  using Precision = double;
+  enum CycleType { VCYCLE = MAD_VCYCLE, FMG = MAD_FMG, SMOOTHER = MAD_SMOOTHER };  // .h:123
+
+  static Pointer New() { return Pointer(new Self()); }
+  ~MultigridAnisotropicDiffusionImageFilter() { mad_destroy(ctx_); }
+
+  // setters (.h:133-160)
+  void SetCycle(CycleType c) { desc_.cycle = c; }
+  void SetIterationsPerGrid(unsigned int n) { desc_.iterations_per_grid = n; }
+  void SetMaxCycles(unsigned int n) { desc_.max_cycles = n; }
+  void SetNumberOfSteps(unsigned int n) { desc_.number_of_steps = n; }
+  void SetTimeStep(Precision dt) { desc_.time_step = dt; }
+  void SetTolerance(Precision t) { desc_.tolerance = t; }
+  void SetVerbose(bool v) { desc_.verbose = v ? 1 : 0; }
+  // MI355X execution options (no reference counterpart)
+  void SetPrecision(int32_t p) { desc_.precision = p; desc_.stall_guard = (p == MAD_FP32); }
+  void SetDevice(int32_t d) { desc_.device = d; }
+
+  // SetDiffusionTensor (.hxx:66-101): copied and cast to fp64 at call time
+  void SetDiffusionTensor(const InputTensorImageType* t) {
+    const int64_t n = t->NumberOfPixels();
+    constexpr int nc = Dim * (Dim + 1) / 2;
+    tensor_.resize((size_t)n * nc);
+    const auto* src = t->GetBufferPointer();
+    for (int64_t p = 0; p < n; ++p)
+      for (int c = 0; c < nc; ++c) tensor_[(size_t)p * nc + c] = (double)src[p].c[c];
+  }
+  void SetInput(const TInputImage* img) { input_ = img; }
+  typename TOutputImage::Pointer GetOutput() const { return output_; }
+  const mad_stats& GetStats() const { return stats_; }
+
+  // GenerateData (.hxx:104-297), on the GPU through mad_run
+  void Update() {
+    if (!input_ || tensor_.empty()) throw Error(MAD_ERR_STATE, "SetInput and SetDiffusionTensor first");
+    mad_desc d = desc_;
+    d.dim = (int32_t)Dim;
+    for (unsigned q = 0; q < 3; ++q) {
+      d.size[q] = q < Dim ? input_->GetSize()[q] : 1;
+      d.spacing[q] = q < Dim ? input_->GetSpacing()[q] : 1.0;
+    }
+    d.smoother = TSmootherType::id;
+    mad_destroy(ctx_);
+    ctx_ = nullptr;
+    check(mad_create(&d, &ctx_));
+    check(mad_set_tensor(ctx_, tensor_.data(), MAD_F64), ctx_);
+    output_ = TOutputImage::New();
+    output_->SetRegions(input_->GetSize());
+    output_->Allocate();
+    output_->SetSpacing(input_->GetSpacing());
+    output_->SetOrigin(input_->GetOrigin());  // .hxx:286
+    check(mad_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
+                  output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id, &stats_),
+          ctx_);
+  }
+
+ protected:
+  MultigridAnisotropicDiffusionImageFilter() { check(mad_desc_init(&desc_)); }
+
+ private:
+  mad_desc desc_{};
+  mad_ctx* ctx_ = nullptr;
+  mad_stats stats_{};
+  const TInputImage* input_ = nullptr;
+  std::vector<double> tensor_;
+  typename TOutputImage::Pointer output_;
+};
+
+}  // namespace mad
+#endif  // MAD_ITK_HPP

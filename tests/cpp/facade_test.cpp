@@ -1,0 +1,57 @@
+// C++ drop-in check: the ITK-shaped facade (include/mad_itk.hpp) used exactly like
+// test/itk2DDiffusionTest_WJ.cxx:47-109 uses the reference filter.
+//   facade_test host   -> host-only calls (no GPU): defaults + depth rule
+//   facade_test run    -> 2D filter run on the GPU, prints the output checksum
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "mad_itk.hpp"
+
+using ImageType = mad::itkshim::Image<float, 2>;
+using FilterType = mad::MultigridAnisotropicDiffusionImageFilter<
+    ImageType, ImageType, mad::MultigridWeightedJacobiSmoother<2>>;
+
+int main(int argc, char** argv) {
+  const bool run = argc > 1 && std::strcmp(argv[1], "run") == 0;
+  mad_desc d;
+  mad_desc_init(&d);
+  if (d.iterations_per_grid != 2 || d.max_cycles != 100 || d.time_step != 0.01) return 2;
+  const int64_t sz[3] = {256, 256, 1};
+  if (mad_max_depth(2, sz) != 5) return 3;
+  if (!run) {
+    std::printf("host ok\n");
+    return 0;
+  }
+  auto input = ImageType::New();
+  input->SetRegions({64, 48});
+  input->Allocate();
+  input->SetSpacing({1.0, 1.0});
+  for (int64_t i = 0; i < input->NumberOfPixels(); ++i)
+    input->GetBufferPointer()[i] = (float)(128.0 + 60.0 * std::sin(0.1 * (double)i));
+  auto tensor = FilterType::InputTensorImageType::New();
+  tensor->SetRegions({64, 48});
+  tensor->Allocate();
+  for (int64_t i = 0; i < tensor->NumberOfPixels(); ++i) {
+    auto& t = tensor->GetBufferPointer()[i];
+    t(0, 0) = 50.f;  // itk2DDiffusionTest_GS.cxx:65-70
+    t(1, 1) = 30.f;
+    t(0, 1) = 0.f;
+  }
+  auto filter = FilterType::New();
+  filter->SetInput(input.get());
+  filter->SetDiffusionTensor(tensor.get());
+  filter->SetIterationsPerGrid(2);
+  filter->SetTimeStep(0.1);
+  filter->SetNumberOfSteps(1);
+  filter->SetMaxCycles(100);
+  filter->SetTolerance(1e-6);
+  filter->SetCycle(FilterType::VCYCLE);
+  filter->Update();
+  double sum = 0.0;
+  auto out = filter->GetOutput();
+  for (int64_t i = 0; i < out->NumberOfPixels(); ++i) sum += out->GetBufferPointer()[i];
+  std::printf("run ok cycles=%u relres=%.3e checksum=%.6f\n", filter->GetStats().total_cycles,
+              filter->GetStats().last_relres, sum);
+  return filter->GetStats().last_relres <= 1e-6 ? 0 : 4;
+}
