@@ -34,7 +34,8 @@ def parse():
     p.add_argument("--size", type=int, default=512)
     p.add_argument("--vcycles", type=int, default=5)
     p.add_argument("--smoother", default="gs", choices=["gs", "wj"])
-    p.add_argument("--gs-kernel", type=int, default=0, help="0 auto (fused), 1 per-colour passes")
+    p.add_argument("--gs-kernel", type=int, default=0,
+                   help="0 auto (fused v3), 1 per-colour passes, 2 fused v2, 3 fused v3")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -67,11 +68,16 @@ def cpu_baseline(seconds):
                       f"oracle/ (line-faithful restatement of the ITK reference), {el:.1f} s"}
 
 
-def load_traffic(tag):
+def load_traffic(tag, kernel_sig):
+    """Per-launch HBM bytes of the bench kernel from the committed PMC profile
+    (profiles/traffic_<tag>.json, written by tools/parse_prof.py); only used when it
+    was measured on this same kernel instantiation."""
     path = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(path):
         with open(path) as f:
-            return json.load(f)
+            t = json.load(f)
+        if kernel_sig in t.get("kernel", ""):
+            return t
     return None
 
 
@@ -153,12 +159,12 @@ def main():
     units_per_launch = float(shape[0] * shape[1] * shape[2]) / ncolors
     achieved = BYTES_PER_VOXEL_SMOOTH * units_per_launch / (kern_ms * 1e-3) / 1e9
     tag = f"{a.smoother}_{S}"
-    traffic = load_traffic(tag)
+    kname = s.smooth_kernel_name(0)  # as rocprofv3 prints it (profiles/ are matched on it)
+    traffic = load_traffic(tag, kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
             "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "kernel": ("gs_fused_k<float,FULL,64,16,512>" if a.gs_kernel != 1 else
-                       "gs_color_k<float,3,FULL>") if a.smoother == "gs" else "wj_k<float,3,FULL>",
+            "kernel": kname,
             "kernel_ms_mean": round(kern_ms, 5), "launches": launches,
             "algorithmic_bytes_per_launch": BYTES_PER_VOXEL_SMOOTH * units_per_launch}
     if traffic:

@@ -99,8 +99,8 @@ typedef struct mad_desc {
   int32_t tensor_kind;           /* mad_tensor_kind, default AUTO */
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
   int32_t rank;                  /* this rank */
-  int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep),
-                                    1 one launch per colour, 2 fused */
+  int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep, v3),
+                                    1 one launch per colour, 2 fused v2, 3 fused v3 */
   int32_t reserved[8];
 } mad_desc;
 
@@ -199,6 +199,10 @@ int mad_synchronize(mad_ctx *ctx);
  * (sweep) kernel launches.  Used by bench.py. */
 int mad_bench_smooth(mad_ctx *ctx, int32_t level, uint32_t sweeps, double *total_ms,
                      double *kernel_ms_mean, uint32_t *kernel_launches);
+/* Name of the kernel one smoother sweep on `level` launches, as rocprofv3 prints
+ * its template arguments (e.g. "gs_fused3_k<float, 3, 64, 32, 1024, 4, 2>"), so a
+ * profile summary can be matched to the bench line. */
+int mad_smooth_kernel_name(mad_ctx *ctx, int32_t level, char *buf, int32_t len);
 /* Time `cycles` V-cycles (device time). */
 int mad_bench_vcycle(mad_ctx *ctx, uint32_t cycles, double *total_ms);
 /* Deterministic synthetic inputs generated on the device (bench / smoke):

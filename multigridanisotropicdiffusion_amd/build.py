@@ -34,7 +34,7 @@ def build(force=False, verbose=True):
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-o", OUT + ".tmp"]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-lrccl"]
+    cmd += ["-lrccl", "-lrocsolver", "-lrocblas"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=HERE)

@@ -40,9 +40,14 @@ inline int coef_count(int dim, int kind) {
 // Geometry of one level slab as seen by a kernel.  Arrays are x-fastest; the
 // base pointer addresses local plane 0; in 3D GHOST ghost planes are allocated on
 // each side (rank halos; at a global boundary the mirror is used instead).
-// Coefficient fields use an x-parity-split row layout: in every row the even-x
-// points come first, then the odd-x points (cidx below), so each colour class of
-// a row is one contiguous run.
+// Coefficient fields are stored point-interleaved (AoS): the NCF coefficients of a
+// point are contiguous, so one point is one 16/24/36-byte record (fp32) read with
+// wide loads, and a run of points of one colour is one contiguous byte range
+// (a tile halo then costs at most a line at each end of a run, not one per field).
+// Points are ordered x-parity split within every row: the even-x points first,
+// then the odd-x points (cidx below), so each colour class of a row is one run.
+// 3D levels keep GHOST coefficient planes below and above the slab (neighbour data
+// on rank slabs, padding for masked border lanes otherwise).
 constexpr int GHOST = 4;
 
 struct Geo {
@@ -53,9 +58,9 @@ struct Geo {
   int hx0;              // (nx + 1) / 2: start of the odd-x half of a coefficient row
   int64_t sy, sz;       // strides
   int64_t N;            // nx*ny*nz (owned points)
-  int64_t cs;           // coefficient field stride (N, + 2*GHOST planes on rank slabs)
 };
 
+// coefficient record index of point (i, j, k): element cidx * NCF + field
 __device__ __forceinline__ int64_t cidx(const Geo& g, int i, int j, int k) {
   return (int64_t)k * g.sz + (int64_t)j * g.sy + ((i & 1) ? g.hx0 + (i >> 1) : (i >> 1));
 }
@@ -76,12 +81,13 @@ template <typename T, int DIM, int KIND>
 __device__ __forceinline__ void coefs_from_raw(const T* raw, const Rat<T>& rat, Coefs<T>& q);
 
 template <typename T, int DIM, int KIND>
-__device__ __forceinline__ void load_coefs(const T* __restrict__ cf, int64_t N, int64_t c,
-                                           const Rat<T>& rat, Coefs<T>& q) {
+__device__ __forceinline__ void load_coefs(const T* __restrict__ cf, int64_t c, const Rat<T>& rat,
+                                           Coefs<T>& q) {
   constexpr int NCF = CoefLayout<DIM, KIND>::N;
+  const T* rec = cf + c * NCF;
   T raw[NCF];
 #pragma unroll
-  for (int a = 0; a < NCF; ++a) raw[a] = cf[a * N + c];
+  for (int a = 0; a < NCF; ++a) raw[a] = rec[a];
   coefs_from_raw<T, DIM, KIND>(raw, rat, q);
 }
 
@@ -93,21 +99,27 @@ __device__ __forceinline__ void load_coefs(const T* __restrict__ cf, int64_t N, 
 // function, so the fused and the per-colour GS kernels are bit-identical.
 template <typename T, int DIM, int KIND>
 __device__ __forceinline__ void stencil_combine(const Coefs<T>& q, const T* nb, T& D, T& S) {
-  T s = (q.ax + q.gx) * nb[0] + (q.ax - q.gx) * nb[1] + (q.ay + q.gy) * nb[2] +
-        (q.ay - q.gy) * nb[3];
-  T d = T(1) + T(2) * (q.ax + q.ay);
+  // explicit fma chain with contraction off: every kernel (per-colour, fused,
+  // Jacobi, residual) rounds this expression identically whatever the context
+#pragma clang fp contract(off)
+  T s = (q.ax + q.gx) * nb[0];
+  s = fma(q.ax - q.gx, nb[1], s);
+  s = fma(q.ay + q.gy, nb[2], s);
+  s = fma(q.ay - q.gy, nb[3], s);
+  T d = T(2) * (q.ax + q.ay);
   if (DIM == 3) {
-    s += (q.az + q.gz) * nb[4] + (q.az - q.gz) * nb[5];
-    d += T(2) * q.az;
+    s = fma(q.az + q.gz, nb[4], s);
+    s = fma(q.az - q.gz, nb[5], s);
+    d = fma(T(2), q.az, d);
   }
   if (KIND == KFULL) {
-    s += q.exy * (nb[6] - nb[7] - nb[8] + nb[9]);
+    s = fma(q.exy, (nb[6] - nb[7]) - (nb[8] - nb[9]), s);
     if (DIM == 3) {
-      s += q.exz * (nb[10] - nb[11] - nb[12] + nb[13]);
-      s += q.eyz * (nb[14] - nb[15] - nb[16] + nb[17]);
+      s = fma(q.exz, (nb[10] - nb[11]) - (nb[12] - nb[13]), s);
+      s = fma(q.eyz, (nb[14] - nb[15]) - (nb[16] - nb[17]), s);
     }
   }
-  D = d;
+  D = T(1) + d;
   S = s;
 }
 
@@ -158,7 +170,7 @@ __device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* 
                                               const Geo& g, const Rat<T>& rat, int i, int j,
                                               int k, int64_t p, T& D, T& S) {
   Coefs<T> q;
-  load_coefs<T, DIM, KIND>(cf, g.cs, cidx(g, i, j, k), rat, q);
+  load_coefs<T, DIM, KIND>(cf, cidx(g, i, j, k), rat, q);
   T nb[18];
   gather_nb<T, DIM, KIND>(u, g, i, j, k, p, nb);
   stencil_combine<T, DIM, KIND>(q, nb, D, S);
@@ -259,6 +271,64 @@ __device__ __forceinline__ void coefs_from_raw(const T* raw, const Rat<T>& rat, 
   }
 }
 
+// raw buffer access (gfx9 descriptor, no range limit): uniform base in SGPRs,
+// 32-bit per-lane byte offset + uniform byte offset -> no VALU address arithmetic
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+  } else {
+    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    return __builtin_bit_cast(T, v);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  if constexpr (sizeof(T) == 4) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, 0, 0);
+  } else {
+    using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, (int)voff, 0, 0);
+  }
+}
+
+// one coefficient record (NCF values of T) at byte offset voff: dword x3 chunks when
+// the record is a multiple of 12 bytes, else x4 chunks + remainder
+template <typename T, int NCF>
+__device__ __forceinline__ void buf_load_rec(__amdgpu_buffer_rsrc_t r, uint32_t voff, T* out) {
+  constexpr int NB = NCF * (int)sizeof(T);
+  constexpr int NW = NB / 4;
+  uint32_t w[NW];
+  // chunk offsets go in soffset (inline constants), so no VALU add per chunk
+  if constexpr (NB % 12 == 0 && NB % 16 != 0) {
+#pragma unroll
+    for (int q = 0; q < NW / 3; ++q) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 12 * q, 0);
+      w[3 * q] = v[0]; w[3 * q + 1] = v[1]; w[3 * q + 2] = v[2];
+    }
+  } else {
+    int q = 0;
+#pragma unroll
+    for (; q + 4 <= NW; q += 4) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 4 * q, 0);
+      w[q] = v[0]; w[q + 1] = v[1]; w[q + 2] = v[2]; w[q + 3] = v[3];
+    }
+    if constexpr (NW % 4 == 3) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 4 * (NW - 3), 0);
+      w[NW - 3] = v[0]; w[NW - 2] = v[1]; w[NW - 1] = v[2];
+    } else if constexpr (NW % 4 == 2) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 4 * (NW - 2), 0);
+      w[NW - 2] = v[0]; w[NW - 1] = v[1];
+    } else if constexpr (NW % 4 == 1) {
+      w[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 4 * (NW - 1), 0);
+    }
+  }
+  __builtin_memcpy(out, w, NB);
+}
+
 template <int NC, int TX, int TY>
 struct FusedGeom {
   static constexpr int H = NC;
@@ -305,7 +375,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
   const int ry0 = tyi * TY - H;
   const int tid = threadIdx.x;
   const int nx = g.nx, ny = g.ny, sy = (int)g.sy;
-  const int64_t sz = g.sz, NF = g.cs;
+  const int64_t sz = g.sz;
 
   const int zlo = g.zlo_ghost ? -GHOST : 0;          // loadable planes [zlo, zhi)
   const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;
@@ -379,10 +449,10 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
     int li, lj;
     if (stage_on(c, m) && locate(c, m, li, lj)) {
       const int gi = rx0 + li, gj = ry0 + lj;
-      const T* cp = cf + (int64_t)m * sz;
+      const T* cp = cf + (int64_t)m * sz * NCF;
       const int co = gj * sy + ((gi & 1) ? g.hx0 + (gi >> 1) : (gi >> 1));
 #pragma unroll
-      for (int a = 0; a < NCF; ++a) raw[c][a] = cp[a * NF + co];
+      for (int a = 0; a < NCF; ++a) raw[c][a] = cp[(int64_t)co * NCF + a];
       bv[c] = b[(int64_t)m * sz + gj * sy + gi];
     }
   };
@@ -463,6 +533,309 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
         const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
         const int gi = rx0 + li, gj = ry0 + lj;
         if (q < TX * TY && gi < nx && gj < ny) out[gj * sy + gi] = P[lj * PITCH + (li & 1) * HALF + (li >> 1)];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused multicolour GS sweep, v3: same wavefront / overlapped-tile schedule and the
+// same arithmetic as gs_fused_k (bit-identical results), restructured so the
+// per-step instruction stream is almost free of address arithmetic:
+//  * the x/y mirror boundary lives in the LDS tile: ghost positions at distance 1
+//    outside the domain hold mirror copies (loaded mirrored, and rewritten when
+//    their source point is updated), so every neighbour read is a ds_read with a
+//    compile-time offset;
+//  * the z loop is unrolled by two with the plane parity normalised, so every
+//    stage point's parity, LDS offset and global offset are compile-time plus one
+//    per-thread constant;
+//  * global loads use a uniform (SGPR) base + 32-bit per-thread byte offset; points
+//    outside the domain load from the padded allocation and are masked at the store.
+// Needs: coefficient fields with >= 1 padding plane below and above every field
+// (LevelData::cf, GHOST planes) and x/b arrays with their GHOST planes; nx, ny >= 3.
+// LDS: dynamic, NP * PLANE * sizeof(T) bytes.
+template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2>
+__global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
+                                                        const T* __restrict__ b, const T* __restrict__ cf,
+                                                        Geo g, Rat<T> rat, int zc, int ntx, int nty) {
+  constexpr int NC = (KIND == KFULL) ? 4 : 2;
+  using FG = FusedGeom<NC, TX, TY>;
+  constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
+  constexpr int PLANE = FG::PLANE, NP = FG::NP;
+  constexpr int UPT = (RX * RY + NT - 1) / NT;
+  constexpr int OPT = (TX * TY + NT - 1) / NT;
+  constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr uint32_t TS = sizeof(T);
+  static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
+  static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
+  extern __shared__ __align__(16) unsigned char fused_smem[];
+  T* lds = reinterpret_cast<T*>(fused_smem);
+
+  int bid = blockIdx.x;
+  {
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = bid & 7, idx = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int tiles = ntx * nty;
+  const int chunk = bid / tiles;
+  const int tile = bid - chunk * tiles;
+  const int tyi = tile / ntx;
+  const int txi = tile - tyi * ntx;
+  const int rx0 = txi * TX - H;
+  const int ry0 = tyi * TY - H;
+  const int tid = threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+  const int sy = (int)g.sy, hx0 = g.hx0;
+  const int64_t sz = g.sz;
+  // tile whose region keeps >= 2 points from every x/y face: no masks, no ghost images
+  const bool interior = rx0 >= 2 && rx0 + RX <= nx - 2 && ry0 >= 2 && ry0 + RY <= ny - 2;
+
+  const int zlo = g.zlo_ghost ? -GHOST : 0;
+  const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;
+  const int ulo = g.zlo_ghost ? -(GHOST - 1) : 0;
+  const int uhi = g.zhi_ghost ? g.nz + GHOST - 1 : g.nz;
+  const int z0 = chunk * zc;
+  const int z1 = min(z0 + zc, g.nz);
+  // first step with its plane parity normalised to even (global z), last step
+  const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + g.zoff) & 1);
+  const int kend = z1 + NC - 2;
+
+  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
+
+  // Plane-load and output element offsets are recomputed every step from an opaque
+  // copy of the thread index (tq): keeping them resident costs 12 VGPRs, which
+  // pushes the kernel past 128 and into scratch spills that miss L2.
+  int tq = tid;
+  auto u_src = [&](int e) -> uint32_t {
+    const int q = tq + e * NT;
+    const int lj = q / RX, li = q - (q / RX) * RX;
+    int gi = rx0 + li, gj = ry0 + lj;
+    if (!interior) {
+      gi = mirror(gi, nx);
+      gj = mirror(gj, ny);
+    }
+    return (uint32_t)(gj * sy + gi) * TS;
+  };
+  auto u_dst = [&](int e) -> int {
+    const int q = tq + e * NT;
+    const int lj = q / RX, li = q - (q / RX) * RX;
+    return (q < RX * RY) ? (int)((lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS) : -1;
+  };
+
+  // ---- stage points.  Stage c covers rows/cols of its colour in the region shrunk
+  // by H - (NC-1-c) = c+1 on each side.  For plane parity PM:
+  //   NC=4: li = c+1 + (1^PM) + 2t,  lj = c+1 + yb(c,PM) + 2r
+  //   NC=2: lj = c+1 + r,            li = c+1 + ((c^PM^r)&1) + 2t
+  // Per-thread byte offsets: LDS (within a plane slot), coefficient record (from
+  // the tile's record base ry0*sy + rx0/2), rhs (from ry0*sy + rx0).
+  // NC=4 keeps only the PM=0 offsets: PM=1 moves every point by a uniform delta
+  // (pdelta below), so it is folded into the uniform bases.
+  constexpr int NPM = (NC == 4) ? 1 : 2;
+  uint32_t pl[NC][NPM], pg[NC][NPM], pb[NC][NPM];
+  uint32_t vmask = 0, gmask = 0;  // bit (c*2+PM): valid point; 4 ghost-image bits each
+  uint32_t omask = 0;              // bit (c*2+PM): li odd (per thread only for NC=2)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int cols = FG::cols(c);
+    const bool has = tid < FG::rows(c) * cols;
+    const int r = has ? tid / cols : 0;
+    const int t = has ? tid - (tid / cols) * cols : 0;
+    const int l0 = c + 1;
+#pragma unroll
+    for (int PM = 0; PM < 2; ++PM) {
+      int li, lj;
+      if (NC == 4) {
+        li = l0 + (1 ^ PM) + 2 * t;
+        lj = l0 + (((c >> 1) ^ PM ^ l0) & 1) + 2 * r;
+      } else {
+        lj = l0 + r;
+        li = l0 + ((c ^ PM ^ r) & 1) + 2 * t;
+      }
+      const int gi = rx0 + li, gj = ry0 + lj;
+      const bool ok = has && gi >= 0 && gi < nx && gj >= 0 && gj < ny;
+      vmask |= (ok ? 1u : 0u) << (c * 2 + PM);
+      const uint32_t gb = (ok && gi == 1 ? 1u : 0u) | (ok && gi == nx - 2 ? 2u : 0u) |
+                          (ok && gj == 1 ? 4u : 0u) | (ok && gj == ny - 2 ? 8u : 0u);
+      gmask |= gb << (4 * (c * 2 + PM));
+      omask |= (uint32_t)(li & 1) << (c * 2 + PM);
+      if (PM < NPM) {
+        pl[c][PM] = (uint32_t)(lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS;
+        pg[c][PM] = (uint32_t)(lj * sy + (li & 1) * hx0 + (li >> 1)) * (TS * NCF);
+        pb[c][PM] = (uint32_t)(lj * sy + li) * TS;
+      }
+    }
+  }
+  // NC=4, PM=1 vs PM=0: li -> li-1, lj -> lj + 1 - 2*yb0 (yb0 = ((c>>1) ^ (c+1)) & 1)
+  // deltas: .l LDS elements (compile-time), .g coefficient records, .b rhs elements
+  struct PD {
+    int l;
+    int64_t g, b;
+  };
+  auto pdelta = [&](int c, int PM) -> PD {
+    if (NC != 4 || PM == 0) return PD{0, 0, 0};
+    const int dy = 1 - 2 * (((c >> 1) ^ (c + 1)) & 1);
+    const bool odd0 = (c & 1) != 0;  // li parity at PM=0: (c+2) & 1
+    return PD{dy * PITCH + (odd0 ? -HALF : HALF - 1), (int64_t)dy * sy + (odd0 ? -hx0 : hx0 - 1),
+              (int64_t)dy * sy - 1};
+  };
+  const int64_t cbase = (int64_t)ry0 * sy + (rx0 >> 1);  // rx0 is even
+  const int64_t bbase = (int64_t)ry0 * sy + rx0;
+
+  auto slot = [](int m) { return (m + NP * 64) % NP; };
+  auto plane_ok = [&](int m) { return m >= zlo && m < zhi; };
+  auto stage_on = [&](int c, int m) {
+    const int h = NC - 1 - c;
+    return m >= z0 - h && m < z1 + h && m >= ulo && m < uhi;
+  };
+  unsigned char* lbytes = fused_smem;
+
+  T up[UPT];
+  T raw[NC][NCF];
+  T bv[NC];
+  auto load_plane = [&](int m) {
+    m = min(max(m, zlo), zhi - 1);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src(e), 0u);
+  };
+  auto put_plane = [&](int m) {
+    unsigned char* P = lbytes + slot(m) * (PLANE * TS);
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) {
+      const int d = u_dst(e);
+      if (e < UPT - 1 || d >= 0) *reinterpret_cast<T*>(P + d) = up[e];
+    }
+  };
+  // stage c data of step k (plane m = k - c, parity PM)
+  // unconditional (the plane index clamped into the loadable range): a conditional
+  // load makes the compiler copy every prefetch register at the join
+  auto load_stage = [&](int c, int k, int PM) {
+    const int m = min(max(k - c, zlo), zhi - 1);
+    {
+      const PD d = pdelta(c, PM);
+      buf_load_rec<T, NCF>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * NCF), pg[c][PM % NPM],
+                           raw[c]);
+      bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
+    }
+  };
+  auto stage = [&](int c, int k, int PM) {
+    const int m = k - c;
+    if (!stage_on(c, m)) return;
+    const int zm = (m == 0 && !g.zlo_ghost) ? 1 : m - 1;
+    const int zp = (m == g.nz - 1 && !g.zhi_ghost) ? g.nz - 2 : m + 1;
+    const uint32_t o = pl[c][PM % NPM] + (uint32_t)(pdelta(c, PM).l * (int)TS);
+    unsigned char* A0 = lbytes + slot(m) * (PLANE * TS) + o;
+    const unsigned char* Am = lbytes + slot(zm) * (PLANE * TS) + o;
+    const unsigned char* Ap = lbytes + slot(zp) * (PLANE * TS) + o;
+    // li parity: NC=4 compile-time ((c+1+(1^PM)) & 1); NC=2 per thread (row parity)
+    bool odd;
+    if (NC == 4) {
+      odd = ((c + 1 + (1 ^ PM)) & 1) != 0;
+    } else {
+      odd = ((omask >> (c * 2 + PM)) & 1u) != 0;
+    }
+    const int ox_p = odd ? 1 - HALF : HALF;
+    const int ox_m = odd ? -HALF : HALF - 1;
+    auto rd = [](const unsigned char* p, int off) { return *reinterpret_cast<const T*>(p + off * (int)TS); };
+    T nb[18];
+    nb[0] = rd(A0, ox_p);
+    nb[1] = rd(A0, ox_m);
+    nb[2] = rd(A0, PITCH);
+    nb[3] = rd(A0, -PITCH);
+    nb[4] = rd(Ap, 0);
+    nb[5] = rd(Am, 0);
+    if (KIND == KFULL) {
+      nb[6] = rd(A0, ox_p + PITCH);
+      nb[7] = rd(A0, ox_p - PITCH);
+      nb[8] = rd(A0, ox_m + PITCH);
+      nb[9] = rd(A0, ox_m - PITCH);
+      nb[10] = rd(Ap, ox_p);
+      nb[11] = rd(Am, ox_p);
+      nb[12] = rd(Ap, ox_m);
+      nb[13] = rd(Am, ox_m);
+      nb[14] = rd(Ap, PITCH);
+      nb[15] = rd(Am, PITCH);
+      nb[16] = rd(Ap, -PITCH);
+      nb[17] = rd(Am, -PITCH);
+    }
+    Coefs<T> q;
+    coefs_from_raw<T, 3, KIND>(raw[c], rat, q);
+    T D, S;
+    stencil_combine<T, 3, KIND>(q, nb, D, S);
+    const T v = (bv[c] + S) / D;
+    const int bit = c * 2 + PM;
+    if (interior) {
+      if (NC == 2 || FG::rows(c) * FG::cols(c) < NT) {
+        if ((vmask >> bit) & 1u) *reinterpret_cast<T*>(A0) = v;
+      } else {
+        *reinterpret_cast<T*>(A0) = v;
+      }
+    } else if ((vmask >> bit) & 1u) {
+      *reinterpret_cast<T*>(A0) = v;
+      const uint32_t gb = (gmask >> (4 * bit)) & 15u;
+      if (gb) {
+        // mirror images u~(-1) = u(1), u~(n) = u(n-2): same row parity, +-1 in the half
+        // row (x) and +-2 rows (y); corners need both
+        const int xs[3] = {0, (gb & 1u) ? -1 : 0, (gb & 2u) ? 1 : 0};
+        const int ys[3] = {0, (gb & 4u) ? -2 * PITCH : 0, (gb & 8u) ? 2 * PITCH : 0};
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+          for (int bq = 0; bq < 3; ++bq) {
+            if ((a == 0 && bq == 0) || (a > 0 && xs[a] == 0) || (bq > 0 && ys[bq] == 0)) continue;
+            *reinterpret_cast<T*>(A0 + (xs[a] + ys[bq]) * (int)TS) = v;
+          }
+      }
+    }
+  };
+
+  // prologue: planes kbeg-1, kbeg into LDS; plane kbeg+1 and step kbeg's stage data
+  for (int m = kbeg - 1; m <= kbeg; ++m)
+    if (plane_ok(m)) {
+      load_plane(m);
+      put_plane(m);
+    }
+  load_plane(kbeg + 1);
+#pragma unroll
+  for (int c = 0; c < LEAD; ++c) load_stage(c, kbeg, c & 1);
+
+  for (int k0 = kbeg; k0 <= kend; k0 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = k0 + u;
+      if (k <= kend) {
+        // keep the per-thread masks in VGPRs: without this the compiler hoists every
+        // (stage, parity, flag) test out of the loop as a 64-bit lane mask and spills
+        asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(omask), "+v"(tq));
+        if (plane_ok(k + 1)) put_plane(k + 1);
+        load_plane(k + 2);
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          stage(c, k, (u ^ c) & 1);
+          // prefetch LEAD stages ahead: (k, c) + LEAD -> (k + dk, c2); raw[c2] was
+          // last read at (k + dk - 1, c2), before this point
+          {
+            constexpr int L = LEAD < NC ? LEAD : NC;
+            const int c2 = (c + L) % NC, dk = (c + L) / NC;
+            load_stage(c2, k + dk, (u ^ dk ^ c2) & 1);
+          }
+          __syncthreads();
+        }
+        const int mo = k - NC + 1;
+        if (mo >= z0 && mo < z1) {
+          const unsigned char* P = lbytes + slot(mo) * (PLANE * TS);
+          const __amdgpu_buffer_rsrc_t ro = buf_rsrc(uout + (int64_t)mo * sz);
+#pragma unroll
+          for (int e = 0; e < OPT; ++e) {
+            const int q = tq + e * NT;
+            const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
+            const int gi = rx0 + li, gj = ry0 + lj;
+            if (q < TX * TY && gi < nx && gj < ny)
+              buf_store<T>(*reinterpret_cast<const T*>(P + (lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS),
+                           ro, (uint32_t)(gj * sy + gi) * TS);
+          }
+        }
       }
     }
   }
@@ -811,8 +1184,8 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
   if (i >= nx || j >= ny) return;
   const int64_t n = (int64_t)nx * ny * nz;
   const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
-  // output index in the x-parity-split coefficient layout
-  const int64_t o = (int64_t)nx * (j + (int64_t)ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1));
+  // output record in the point-interleaved, x-parity-split coefficient layout (cidx)
+  const int64_t o = ((int64_t)nx * (j + (int64_t)ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * L::N;
   const double h[3] = {hx, hy, hz};
   const int nn[3] = {nx, ny, nz};
   const int id[3] = {i, j, k};
@@ -820,19 +1193,19 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
   if (KIND == KISO) {
     cf[o] = (T)(dt * M[p] / (h[0] * h[0]));
   } else {
-    for (int d = 0; d < DIM; ++d) cf[d * n + o] = (T)(dt * M[tcomp(DIM, d, d) * n + p] / (h[d] * h[d]));
+    for (int d = 0; d < DIM; ++d) cf[o + d] = (T)(dt * M[tcomp(DIM, d, d) * n + p] / (h[d] * h[d]));
   }
   for (int d = 0; d < DIM; ++d) {
     double s = 0.0;
     for (int d2 = 0; d2 < DIM; ++d2)
       s += delta_f(M + tcomp(DIM, d, d2) * n, p, id[d2], nn[d2], st[d2]) / (2.0 * h[d2]);
-    cf[(L::NA + d) * n + o] = (T)(dt / (2.0 * h[d]) * s);
+    cf[o + L::NA + d] = (T)(dt / (2.0 * h[d]) * s);
   }
   if (KIND == KFULL) {
     int e = L::NA + L::NG;
     for (int d = 0; d < DIM; ++d)
       for (int d2 = d + 1; d2 < DIM; ++d2, ++e)
-        cf[e * n + o] = (T)(dt * M[tcomp(DIM, d, d2) * n + p] / (2.0 * h[d] * h[d2]));
+        cf[o + e] = (T)(dt * M[tcomp(DIM, d, d2) * n + p] / (2.0 * h[d] * h[d2]));
   }
 }
 

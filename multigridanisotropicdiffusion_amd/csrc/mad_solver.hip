@@ -12,11 +12,14 @@
 // Everything runs on one HIP stream per context; level arrays stay resident in
 // HBM across V-cycles and time steps; only norms cross PCIe (8 bytes/cycle).
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -115,61 +118,34 @@ int max_depth_rule(int dim, const int64_t n0[3]) {
 }
 
 // ---------------------------------------------------------------------------
-// dense fp64 LU (partial pivoting) + explicit inverse of the coarsest operator
-// (replaces vnl_sparse_lu, DS.hxx:81-86; the inverse turns each per-cycle solve
-// into one device GEMV)
-bool invert_dense(int64_t n, std::vector<double>& a, std::vector<double>& inv) {
-  std::vector<int64_t> piv(n);
-  for (int64_t k = 0; k < n; ++k) {
-    int64_t p = k;
-    double best = std::fabs(a[k * n + k]);
-    for (int64_t i = k + 1; i < n; ++i)
-      if (std::fabs(a[i * n + k]) > best) { best = std::fabs(a[i * n + k]); p = i; }
-    piv[k] = p;
-    if (best == 0.0) return false;
-    if (p != k)
-      for (int64_t j = 0; j < n; ++j) std::swap(a[k * n + j], a[p * n + j]);
-    const double ip = 1.0 / a[k * n + k];
-    for (int64_t i = k + 1; i < n; ++i) {
-      const double f = a[i * n + k] * ip;
-      a[i * n + k] = f;
-      if (f != 0.0) {
-        const double* rk = &a[k * n];
-        double* ri = &a[i * n];
-        for (int64_t j = k + 1; j < n; ++j) ri[j] -= f * rk[j];
-      }
-    }
-  }
-  inv.assign((size_t)n * n, 0.0);
-  // columns of the inverse solved in parallel (setup only)
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  auto work = [&](unsigned t) {
-    std::vector<double> x(n);
-    for (int64_t c = t; c < n; c += nt) {
-      std::fill(x.begin(), x.end(), 0.0);
-      x[c] = 1.0;
-      for (int64_t k = 0; k < n; ++k)
-        if (piv[k] != k) std::swap(x[k], x[piv[k]]);
-      for (int64_t i = 0; i < n; ++i) {
-        double s = x[i];
-        const double* ri = &a[i * n];
-        for (int64_t j = 0; j < i; ++j) s -= ri[j] * x[j];
-        x[i] = s;
-      }
-      for (int64_t i = n - 1; i >= 0; --i) {
-        double s = x[i];
-        const double* ri = &a[i * n];
-        for (int64_t j = i + 1; j < n; ++j) s -= ri[j] * x[j];
-        x[i] = s / ri[i];
-      }
-      for (int64_t r = 0; r < n; ++r) inv[r * n + c] = x[r];
-    }
-  };
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& t : th) t.join();
-  return true;
+// dense fp64 LU (partial pivoting) + explicit inverse of the coarsest operator on
+// the device (rocSOLVER getrf + getri; replaces vnl_sparse_lu, DS.hxx:81-86; the
+// inverse turns each per-cycle solve into one device GEMV).  `a` is row-major A,
+// which rocSOLVER reads as column-major A^T: inv(A^T) column-major is inv(A)
+// row-major, so the result needs no transpose.  Returns false if A is singular.
+bool invert_dense_device(int64_t n, const std::vector<double>& a, double* d_inv,
+                         hipStream_t stream) {
+  rocblas_handle h = nullptr;
+  if (rocblas_create_handle(&h) != rocblas_status_success)
+    throw std::runtime_error("rocblas_create_handle failed");
+  rocblas_set_stream(h, stream);
+  rocblas_int* ipiv = nullptr;
+  rocblas_int* info = nullptr;
+  HIP_CHECK(hipMalloc(&ipiv, sizeof(rocblas_int) * n));
+  HIP_CHECK(hipMalloc(&info, sizeof(rocblas_int) * 2));
+  HIP_CHECK(hipMemcpyAsync(d_inv, a.data(), sizeof(double) * n * n, hipMemcpyHostToDevice, stream));
+  const rocblas_int N = (rocblas_int)n;
+  rocblas_status st = rocsolver_dgetrf(h, N, N, d_inv, N, ipiv, info);
+  if (st == rocblas_status_success) st = rocsolver_dgetri(h, N, d_inv, N, ipiv, info + 1);
+  rocblas_int hinfo[2] = {0, 0};
+  HIP_CHECK(hipMemcpyAsync(hinfo, info, sizeof hinfo, hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  HIP_CHECK(hipFree(ipiv));
+  HIP_CHECK(hipFree(info));
+  rocblas_destroy_handle(h);
+  if (st != rocblas_status_success)
+    throw std::runtime_error("rocsolver getrf/getri failed (status " + std::to_string((int)st) + ")");
+  return hinfo[0] == 0 && hinfo[1] == 0;
 }
 
 }  // namespace
@@ -218,6 +194,7 @@ struct SolverBase {
                             unsigned* launches) = 0;
   virtual void bench_vcycle(unsigned n, double* total_ms) = 0;
   virtual void synth_level(int l, int which, uint64_t seed) = 0;
+  virtual std::string smooth_kernel(int l) = 0;
 };
 
 mad_ctx::~mad_ctx() {
@@ -276,22 +253,28 @@ class Solver final : public SolverBase {
       L.rat.r[1] = (T)((G.h[0] * G.h[0]) / (G.h[1] * G.h[1]));
       L.rat.r[2] = (T)((G.h[0] * G.h[0]) / (G.h[2] * G.h[2]));
       L.ghost = (dim == 3) ? (int64_t)GHOST * L.g.sz : 0;
-      const int64_t tot = L.g.N + 2 * L.ghost;
+      // + a margin of rows at both ends: the fused sweep's masked border lanes read
+      // up to a tile halo outside the outermost (ghost) plane
+      const int64_t margin = margin_elems(L.g);
+      const int64_t tot = L.g.N + 2 * (L.ghost + margin);
       for (int a = 0; a < 4; ++a) {
         HIP_CHECK(hipMalloc(&L.alloc[a], sizeof(T) * tot));
         HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
       }
-      L.x = L.alloc[0] + L.ghost;
-      L.b = L.alloc[1] + L.ghost;
-      L.r = L.alloc[2] + L.ghost;
-      L.t = L.alloc[3] + L.ghost;
-      // coefficient fields: rank slabs keep GHOST planes per side (the fused sweep
-      // recomputes colours on the ghost planes, csrc/mad_kernels.hpp gs_fused_k)
-      const int64_t cg = G.distributed ? (int64_t)GHOST * L.g.sz : 0;
-      L.g.cs = L.g.N + 2 * cg;
-      HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * L.g.cs * ncoef_));
-      HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * L.g.cs * ncoef_, c->stream));
-      L.cf = L.cf_alloc + cg;
+      L.x = L.alloc[0] + margin + L.ghost;
+      L.b = L.alloc[1] + margin + L.ghost;
+      L.r = L.alloc[2] + margin + L.ghost;
+      L.t = L.alloc[3] + margin + L.ghost;
+      // coefficient records, point-interleaved (mad_kernels.hpp, cidx); 3D levels keep
+      // GHOST coefficient planes per side: neighbour planes on rank slabs (the fused
+      // sweep recomputes colours on them), padding for masked border lanes otherwise
+      const int64_t cplane = L.g.sz * ncoef_;
+      const int64_t cgp = (dim == 3) ? GHOST : 0;
+      const int64_t cmargin = margin * ncoef_;
+      const int64_t ctot = (L.g.nz + 2 * cgp) * cplane + 2 * cmargin;
+      HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * ctot));
+      HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
+      L.cf = L.cf_alloc + cmargin + cgp * cplane;
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
@@ -358,12 +341,110 @@ class Solver final : public SolverBase {
                              std::is_same<T, double>::value, c_->stream);
   }
 
+  // rows kept beyond the outermost plane of every level array (see setup)
+  // (covers a tile region of up to 40 rows x 256 points hanging over the last plane)
+  static int64_t margin_elems(const Geo& g) { return 48 * g.sy + 512; }
+
   bool use_fused(int l) const {
-    const int v = c_->d.gs_kernel;  // 0 auto, 1 per-colour passes, 2 fused
+    const int v = c_->d.gs_kernel;  // 0 auto (v3), 1 per-colour passes, 2 fused v2, 3 fused v3
     if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL) return false;
     if (v == 1) return false;
     (void)l;
     return true;
+  }
+
+  // fused-sweep launch configuration.  Defaults are the measured best at 512^3;
+  // MAD_FUSED_TILE (0 64x16/512, 1 64x32/1024, 2 128x16/1024, 3 128x8/512),
+  // MAD_FUSED_LEAD (prefetch lead in stages, 2 or 3) and MAD_FUSED_BLOCKS (target
+  // grid size) override them for tuning runs (full-tensor fp32/fp64 only).
+  struct FusedCfg {
+    int tile = 0, lead = 2, blocks = 2048;
+  };
+  // fp32 full tensor: 64x32 tiles of 1024 threads, ~1024 blocks (one per CU slot,
+  // 93 KB LDS); fp64 keeps 64x16/512 (the 64x32 ring would need 186 KB of LDS)
+  static const FusedCfg& fused_cfg() {
+    static FusedCfg c = [] {
+      FusedCfg f;
+      if (sizeof(T) == 4) {
+        f.tile = 1;
+        f.blocks = 1024;
+      }
+      if (const char* e = std::getenv("MAD_FUSED_TILE")) f.tile = std::atoi(e);
+      if (const char* e = std::getenv("MAD_FUSED_LEAD")) f.lead = std::atoi(e);
+      if (const char* e = std::getenv("MAD_FUSED_BLOCKS")) f.blocks = std::max(1, std::atoi(e));
+      return f;
+    }();
+    return c;
+  }
+
+  template <int KD, int TX, int TY, int NT>
+  void launch_fused(LevelData<T>& L, const FusedCfg& fc) {
+    const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
+    const int tiles = ntx * nty;
+    int chunks = (fc.blocks + tiles - 1) / tiles;
+    chunks = std::max(1, std::min(chunks, std::max(1, L.g.nz / 32)));
+    const int zc = (L.g.nz + chunks - 1) / chunks;
+    chunks = (L.g.nz + zc - 1) / zc;
+    const unsigned nb = (unsigned)(tiles * chunks);
+    if (c_->d.gs_kernel == 2) {
+      hipLaunchKernelGGL((gs_fused_k<T, KD, 64, 16, (KD == KFULL ? 512 : 1024), 4>),
+                         dim3((unsigned)(((L.g.nx + 63) / 64) * ((L.g.ny + 15) / 16) * chunks)),
+                         dim3(KD == KFULL ? 512 : 1024), 0, c_->stream, L.x, L.t, L.b, L.cf, L.g,
+                         L.rat, zc, (L.g.nx + 63) / 64, (L.g.ny + 15) / 16);
+      return;
+    }
+    constexpr int NC = (KD == KFULL) ? 4 : 2;
+    using FG = FusedGeom<NC, TX, TY>;
+    constexpr size_t lds = sizeof(T) * FG::NP * FG::PLANE;
+    REQUIRE(lds <= 160 * 1024, MAD_ERR_UNSUPPORTED,
+            "fused GS tile needs " + std::to_string(lds) + " B of LDS (> 160 KiB)");
+    // fp64 doubles the register footprint: 2 waves per SIMD (one 512-thread block per CU,
+    // which is all its LDS allows anyway)
+    constexpr int MW = sizeof(T) == 8 ? 2 : 4;
+    auto run = [&](auto kern) {
+      static bool attr = false;
+      if (!attr) {
+        HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds));
+        attr = true;
+      }
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
+                         zc, ntx, nty);
+    };
+    if (KD == KFULL && fc.lead == 3)
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>);
+    else
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+  }
+
+  // rocprof-style name of the kernel one level-l sweep launches (bench / profiles)
+  std::string smooth_kernel(int l) override {
+    (void)l;
+    const char* tn = sizeof(T) == 4 ? "float" : "double";
+    const int dim = c_->dim, kind = c_->kind;
+    char buf[160];
+    if (c_->d.smoother == MAD_WEIGHTED_JACOBI) {
+      std::snprintf(buf, sizeof buf, "wj_k<%s, %d, %d>", tn, dim, kind);
+    } else if (c_->d.smoother == MAD_GAUSS_SEIDEL_LEX) {
+      std::snprintf(buf, sizeof buf, "gs_lex_plane_k<%s, %d, %d>", tn, dim, kind);
+    } else if (!use_fused(l)) {
+      std::snprintf(buf, sizeof buf, "gs_color_k<%s, %d, %d>", tn, dim, kind);
+    } else if (c_->d.gs_kernel == 2) {
+      std::snprintf(buf, sizeof buf, "gs_fused_k<%s, %d, 64, 16, %d, 4>", tn, kind,
+                    kind == KFULL ? 512 : 1024);
+    } else {
+      const FusedCfg& fc = fused_cfg();
+      int tx = 64, ty = 16, nt = kind == KFULL ? 512 : 1024;
+      if (kind == KFULL) {
+        if (fc.tile == 1) { tx = 64; ty = 32; nt = 1024; }
+        if (fc.tile == 2) { tx = 128; ty = 16; nt = 1024; }
+        if (fc.tile == 3) { tx = 128; ty = 8; nt = 512; }
+      }
+      const int lead = (kind == KFULL && fc.lead == 3) ? 3 : 2;
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d>", tn, kind, tx, ty,
+                    nt, sizeof(T) == 8 ? 2 : 4, lead);
+    }
+    return buf;
   }
 
   // one fused GS sweep x -> t, then swap (gs_fused_k)
@@ -374,24 +455,22 @@ class Solver final : public SolverBase {
       halo(l, L.b, GHOST);
       L.b_halo_ok = true;
     }
-    constexpr int TX = 64, TY = 16;
-    const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
-    const int tiles = ntx * nty;
-    int chunks = (2048 + tiles - 1) / tiles;
-    chunks = std::max(1, std::min(chunks, std::max(1, L.g.nz / 32)));
-    const int zc = (L.g.nz + chunks - 1) / chunks;
-    chunks = (L.g.nz + zc - 1) / zc;
-    const unsigned nb = (unsigned)(tiles * chunks);
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
-    if (c_->kind == KFULL)
-      hipLaunchKernelGGL((gs_fused_k<T, KFULL, TX, TY, 512, 4>), dim3(nb), dim3(512), 0, c_->stream,
-                         L.x, L.t, L.b, L.cf, L.g, L.rat, zc, ntx, nty);
-    else if (c_->kind == KDIAG)
-      hipLaunchKernelGGL((gs_fused_k<T, KDIAG, TX, TY, 1024, 4>), dim3(nb), dim3(1024), 0, c_->stream,
-                         L.x, L.t, L.b, L.cf, L.g, L.rat, zc, ntx, nty);
-    else
-      hipLaunchKernelGGL((gs_fused_k<T, KISO, TX, TY, 1024, 4>), dim3(nb), dim3(1024), 0, c_->stream,
-                         L.x, L.t, L.b, L.cf, L.g, L.rat, zc, ntx, nty);
+    const FusedCfg& fc = fused_cfg();
+    if (c_->kind == KFULL) {
+      if (fc.tile == 1)
+        launch_fused<KFULL, 64, 32, 1024>(L, fc);
+      else if (fc.tile == 2)
+        launch_fused<KFULL, 128, 16, 1024>(L, fc);
+      else if (fc.tile == 3)
+        launch_fused<KFULL, 128, 8, 512>(L, fc);
+      else
+        launch_fused<KFULL, 64, 16, 512>(L, fc);
+    } else if (c_->kind == KDIAG) {
+      launch_fused<KDIAG, 64, 16, 1024>(L, fc);
+    } else {
+      launch_fused<KISO, 64, 16, 1024>(L, fc);
+    }
     if (e1) HIP_CHECK(hipEventRecord(e1, c_->stream));
     HIP_CHECK(hipGetLastError());
     std::swap(L.x, L.t);
@@ -945,14 +1024,13 @@ class Solver final : public SolverBase {
       });
       HIP_CHECK(hipGetLastError());
       if (slab) {
-        // owned planes plus up to GHOST neighbour planes on each side
-        const int64_t plane = G.n[0] * G.n[1];
+        // owned planes plus up to GHOST neighbour planes on each side (whole plane blocks)
         const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
         const int64_t p1 = std::min<int64_t>(G.z1 + GHOST, G.n[2]);
-        for (int a = 0; a < ncoef_; ++a)
-          HIP_CHECK(hipMemcpyAsync(L.cf + a * L.g.cs + (p0 - G.z0) * plane,
-                                   full_cf + a * Ng + p0 * plane, sizeof(T) * (p1 - p0) * plane,
-                                   hipMemcpyDeviceToDevice, c_->stream));
+        const int64_t cplane = L.g.sz * ncoef_;
+        HIP_CHECK(hipMemcpyAsync(L.cf + (p0 - G.z0) * cplane, full_cf + p0 * cplane,
+                                 sizeof(T) * (p1 - p0) * cplane, hipMemcpyDeviceToDevice,
+                                 c_->stream));
         HIP_CHECK(hipStreamSynchronize(c_->stream));
         HIP_CHECK(hipFree(full_cf));
         full_cf = nullptr;
@@ -998,6 +1076,7 @@ class Solver final : public SolverBase {
                 "direct solver (GH.hxx:36-59)");
     const double* cf = coarse_coef64_.data();
     const int na = (kind == KISO) ? 1 : dim;
+    const int nc = coef_count(dim, kind);
     std::vector<double> A((size_t)n * n, 0.0);
     const int64_t nx = G.n[0], ny = G.n[1], nz = G.n[2];
     const double r1 = (G.h[0] * G.h[0]) / (G.h[1] * G.h[1]);
@@ -1006,17 +1085,18 @@ class Solver final : public SolverBase {
       for (int64_t j = 0; j < ny; ++j)
         for (int64_t i = 0; i < nx; ++i) {
           const int64_t p = i + nx * (j + ny * k);
-          // coefficient fields are x-parity split (mad_kernels.hpp, cidx)
-          const int64_t c = nx * (j + ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1));
+          // point-interleaved, x-parity-split records (mad_kernels.hpp, cidx)
+          const double* rec =
+              cf + (nx * (j + ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * nc;
           double a[3], g[3], e[3] = {0, 0, 0};
           if (kind == KISO) {
-            a[0] = cf[c]; a[1] = cf[c] * r1; a[2] = cf[c] * r2;
+            a[0] = rec[0]; a[1] = rec[0] * r1; a[2] = rec[0] * r2;
           } else {
-            for (int d = 0; d < dim; ++d) a[d] = cf[d * n + c];
+            for (int d = 0; d < dim; ++d) a[d] = rec[d];
           }
-          for (int d = 0; d < dim; ++d) g[d] = cf[(na + d) * n + c];
+          for (int d = 0; d < dim; ++d) g[d] = rec[na + d];
           if (kind == KFULL)
-            for (int q = 0; q < dim * (dim - 1) / 2; ++q) e[q] = cf[(na + dim + q) * n + c];
+            for (int q = 0; q < dim * (dim - 1) / 2; ++q) e[q] = rec[na + dim + q];
           const int64_t xm = (i == 0) ? 1 : i - 1, xp = (i == nx - 1) ? nx - 2 : i + 1;
           const int64_t ym = (j == 0) ? 1 : j - 1, yp = (j == ny - 1) ? ny - 2 : j + 1;
           const int64_t zm = (k == 0) ? 1 : k - 1, zp = (k == nz - 1) ? nz - 2 : k + 1;
@@ -1050,10 +1130,9 @@ class Solver final : public SolverBase {
             }
           }
         }
-    std::vector<double> inv;
-    REQUIRE(invert_dense(n, A, inv), MAD_ERR_SINGULAR, "coarsest operator is singular");
     HIP_CHECK(hipMalloc(&inv_, sizeof(double) * n * n));
-    HIP_CHECK(hipMemcpy(inv_, inv.data(), sizeof(double) * n * n, hipMemcpyHostToDevice));
+    REQUIRE(invert_dense_device(n, A, inv_, c_->stream), MAD_ERR_SINGULAR,
+            "coarsest operator is singular");
   }
 
   // ---- distributed -> replicated hand-over (agglomeration of coarse levels)
@@ -1536,6 +1615,13 @@ int mad_bench_smooth(mad_ctx* c, int32_t level, uint32_t sweeps, double* total_m
                REQUIRE(total_ms && kernel_ms_mean && kernel_launches, MAD_ERR_INVALID, "null out");
                unsigned nl = 0; c->solver->bench_smooth(level, sweeps, total_ms, kernel_ms_mean, &nl);
                *kernel_launches = nl);
+}
+
+int mad_smooth_kernel_name(mad_ctx* c, int32_t level, char* buf, int32_t len) {
+  KERNEL_ENTRY(CHECK_LEVEL(level);
+               REQUIRE(buf && len > 0, MAD_ERR_INVALID, "null or empty buffer");
+               const std::string n = c->solver->smooth_kernel(level);
+               std::snprintf(buf, (size_t)len, "%s", n.c_str()));
 }
 
 int mad_bench_vcycle(mad_ctx* c, uint32_t cycles, double* total_ms) {

@@ -226,6 +226,11 @@ class Solver:
                                              ctypes.byref(k), ctypes.byref(n)))
         return t.value, k.value, n.value
 
+    def smooth_kernel_name(self, level=0):
+        buf = ctypes.create_string_buffer(256)
+        self._check(self._L.mad_smooth_kernel_name(self._ctx, level, buf, 256))
+        return buf.value.decode()
+
     def bench_vcycle(self, cycles):
         t = ctypes.c_double()
         self._check(self._L.mad_bench_vcycle(self._ctx, cycles, ctypes.byref(t)))

@@ -22,11 +22,12 @@ def main():
     p.add_argument("--size", type=int, default=512)
     p.add_argument("--sweeps", type=int, default=3)
     p.add_argument("--smoother", default="gs", choices=["gs", "wj"])
+    p.add_argument("--gs-kernel", type=int, default=0)
     a = p.parse_args()
     import multigridanisotropicdiffusion_amd as M
     S = a.size
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
-    s = M.Solver((S, S, S), time_step=0.1, smoother=sm)
+    s = M.Solver((S, S, S), time_step=0.1, smoother=sm, gs_kernel=a.gs_kernel)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
