@@ -100,11 +100,13 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    # MAD_HIP_LIB: an alternative build of the same library (A/B measurements)
+    path = os.environ.get("MAD_HIP_LIB", LIB_PATH)
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} not found: build the HIP library first "
+            f"{path} not found: build the HIP library first "
             "(python -m multigridanisotropicdiffusion_amd.build)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, i32, u32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64, \
         ctypes.c_double
     dp = ctypes.POINTER(ctypes.c_double)

@@ -695,8 +695,14 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   auto load_plane = [&](int m) {
     m = min(max(m, zlo), zhi - 1);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
+#ifdef MAD_PROBE_NO_U  // measurement builds only: drop the solution-plane stream
+    (void)rs;
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) up[e] = T(0);
+#else
 #pragma unroll
     for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src(e), 0u);
+#endif
   };
   auto put_plane = [&](int m) {
     unsigned char* P = lbytes + slot(m) * (PLANE * TS);
@@ -715,7 +721,11 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       const PD d = pdelta(c, PM);
       buf_load_rec<T, NCF>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * NCF), pg[c][PM % NPM],
                            raw[c]);
+#ifdef MAD_PROBE_NO_B  // measurement builds only (tools/probe_builds.sh): drop the rhs stream
+      bv[c] = T(0);
+#else
       bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
+#endif
     }
   };
   auto stage = [&](int c, int k, int PM) {
@@ -931,58 +941,35 @@ __global__ void __launch_bounds__(256) reduce_final_k(const double* __restrict__
 
 // ---------------------------------------------------------------------------
 // inter-grid transfers (itkInterGridOperators.{h,hxx}), gather form, separable.
-// Restriction taps for coarse index I (IGO.h:115-127): vertex interior 1/4,1/2,1/4
-// about 2I, injection at the two ends; cell interior 1/8,3/8,3/8,1/8 on 2I-1..2I+2,
-// left 1/2,3/8,1/8 on 0..2, right 1/8,3/8,1/2 on 2I-1..2I+1.
-__device__ __forceinline__ int restrict_taps(int I, int nc, int cell, int* idx, double* w) {
-  if (!cell) {
-    if (I == 0 || I == nc - 1) {
-      idx[0] = 2 * I; w[0] = 1.0;
-      return 1;
-    }
-    idx[0] = 2 * I - 1; idx[1] = 2 * I; idx[2] = 2 * I + 1;
-    w[0] = 0.25; w[1] = 0.5; w[2] = 0.25;
-    return 3;
-  }
-  if (I == 0) {
-    idx[0] = 0; idx[1] = 1; idx[2] = 2;
-    w[0] = 0.5; w[1] = 0.375; w[2] = 0.125;
-    return 3;
-  }
-  if (I == nc - 1) {
-    idx[0] = 2 * I - 1; idx[1] = 2 * I; idx[2] = 2 * I + 1;
-    w[0] = 0.125; w[1] = 0.375; w[2] = 0.5;
-    return 3;
-  }
-  idx[0] = 2 * I - 1; idx[1] = 2 * I; idx[2] = 2 * I + 1; idx[3] = 2 * I + 2;
-  w[0] = 0.125; w[1] = 0.375; w[2] = 0.375; w[3] = 0.125;
-  return 4;
-}
-
-// Interpolation taps for fine index f (IGO.h:101-113, scatter stencils turned into
-// gathers): vertex f even -> c(f/2), odd -> (c(f/2) + c(f/2+1))/2; cell f=0 -> c(0),
-// f=2nc-1 -> c(nc-1), f=2I -> 3/4 c(I) + 1/4 c(I-1), f=2I+1 -> 3/4 c(I) + 1/4 c(I+1).
-__device__ __forceinline__ int interp_taps(int f, int nc, int cell, int* idx, double* w) {
-  if (!cell) {
-    if ((f & 1) == 0) {
-      idx[0] = f >> 1; w[0] = 1.0;
-      return 1;
-    }
-    idx[0] = f >> 1; idx[1] = (f >> 1) + 1;
-    w[0] = 0.5; w[1] = 0.5;
-    return 2;
-  }
-  const int I = f >> 1;
-  if (f == 0 || f == 2 * nc - 1) {
-    idx[0] = I; w[0] = 1.0;
-    return 1;
-  }
-  idx[0] = I; w[0] = 0.75;
-  idx[1] = (f & 1) ? I + 1 : I - 1; w[1] = 0.25;
-  return 2;
-}
-
 // coarse(I,J,K) = sum w_x w_y w_z fine(...)   (fine: g level geometry, may read ghosts)
+// Taps are written tap by tap with selects (no per-branch array stores: with three
+// branches each storing all four weights, the compiler merged the tap-3 weight
+// wrongly -- observed on gfx950 with ROCm 7.2 -- and the clamped border rows lost
+// their folded 1/8).
+template <typename W>
+__device__ __forceinline__ void rtaps4(int I, int nc, int cell, int* idx, W* w) {
+  const bool endv = !cell && (I == 0 || I == nc - 1);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ic = min(max(2 * I - 1 + t, 0), 2 * nc - 1);      // cell: clamped 2I-1+t
+    const int iv = endv ? 2 * I : (t == 3 ? 2 * I : 2 * I - 1 + t);  // vertex
+    idx[t] = cell ? ic : iv;
+    const W wc = (t == 0 || t == 3) ? W(0.125) : W(0.375);
+    const W wv = endv ? (t == 0 ? W(1) : W(0)) : (t == 1 ? W(0.5) : (t == 3 ? W(0) : W(0.25)));
+    w[t] = cell ? wc : wv;
+  }
+}
+
+template <typename W>
+__device__ __forceinline__ void itaps2(int f, int nc, int cell, int* idx, W* w) {
+  const int I = f >> 1;
+  const bool odd = (f & 1) != 0;
+  idx[0] = I;
+  idx[1] = cell ? (odd ? min(I + 1, nc - 1) : max(I - 1, 0)) : (odd ? I + 1 : I);
+  w[0] = cell ? W(0.75) : (odd ? W(0.5) : W(1));
+  w[1] = cell ? W(0.25) : (odd ? W(0.5) : W(0));
+}
+
 template <typename T, typename A, int DIM>
 __global__ void __launch_bounds__(256) restrict_k(const T* __restrict__ fine, Geo gf,
                                                   T* __restrict__ coarse, Geo gc, int cx, int cy,
@@ -991,20 +978,26 @@ __global__ void __launch_bounds__(256) restrict_k(const T* __restrict__ fine, Ge
   const int J = blockIdx.y * blockDim.y + threadIdx.y;
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
   if (I >= gc.nx || J >= gc.ny) return;
-  int ix[4], iy[4], iz[4];
-  double wx[4], wy[4], wz[4];
-  const int nxn = restrict_taps(I, gc.nx, cx, ix, wx);
-  const int nyn = restrict_taps(J, gc.ny, cy, iy, wy);
-  int nzn = 1;
-  iz[0] = 0; wz[0] = 1.0;
-  if (DIM == 3) nzn = restrict_taps(K, gc.nz, cz, iz, wz);
+  int ix[4], iy[4], iz[4] = {0, 0, 0, 0};
+  A wx[4], wy[4], wz[4] = {A(1), A(0), A(0), A(0)};
+  rtaps4<A>(I, gc.nx, cx, ix, wx);
+  rtaps4<A>(J, gc.ny, cy, iy, wy);
+  if (DIM == 3) rtaps4<A>(K, gc.nz, cz, iz, wz);
   A v = A(0);
-  for (int c = 0; c < nzn; ++c)
-    for (int bq = 0; bq < nyn; ++bq)
-      for (int a = 0; a < nxn; ++a) {
-        const int64_t q = ix[a] + gf.sy * iy[bq] + gf.sz * (int64_t)(iz[c] - fz_shift);
-        v += (A)(wx[a] * wy[bq] * wz[c]) * (A)fine[q];
-      }
+#pragma unroll
+  for (int c = 0; c < (DIM == 3 ? 4 : 1); ++c) {
+    const T* pl = fine + gf.sz * (int64_t)(iz[c] - fz_shift);
+    A vz = A(0);
+#pragma unroll
+    for (int bq = 0; bq < 4; ++bq) {
+      const T* row = pl + gf.sy * iy[bq];
+      A vy = A(0);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) vy += wx[a] * (A)row[ix[a]];
+      vz += wy[bq] * vy;
+    }
+    v += wz[c] * vz;
+  }
   coarse[I + gc.sy * J + gc.sz * K] = (T)v;
 }
 
@@ -1017,18 +1010,23 @@ __global__ void __launch_bounds__(256) interp_k(const T* __restrict__ coarse, Ge
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= gf.nx || j >= gf.ny) return;
-  int ix[2], iy[2], iz[2];
-  double wx[2], wy[2], wz[2];
-  const int nxn = interp_taps(i, gc.nx, cx, ix, wx);
-  const int nyn = interp_taps(j, gc.ny, cy, iy, wy);
-  int nzn = 1;
-  iz[0] = 0; wz[0] = 1.0;
-  if (DIM == 3) nzn = interp_taps(k, gc.nz, cz, iz, wz);
+  int ix[2], iy[2], iz[2] = {0, 0};
+  T wx[2], wy[2], wz[2] = {T(1), T(0)};
+  itaps2<T>(i, gc.nx, cx, ix, wx);
+  itaps2<T>(j, gc.ny, cy, iy, wy);
+  if (DIM == 3) itaps2<T>(k, gc.nz, cz, iz, wz);
   T v = T(0);
-  for (int c = 0; c < nzn; ++c)
-    for (int bq = 0; bq < nyn; ++bq)
-      for (int a = 0; a < nxn; ++a)
-        v += (T)(wx[a] * wy[bq] * wz[c]) * coarse[ix[a] + gc.sy * iy[bq] + gc.sz * iz[c]];
+#pragma unroll
+  for (int c = 0; c < (DIM == 3 ? 2 : 1); ++c) {
+    const T* pl = coarse + gc.sz * (int64_t)iz[c];
+    T vz = T(0);
+#pragma unroll
+    for (int bq = 0; bq < 2; ++bq) {
+      const T* row = pl + gc.sy * iy[bq];
+      vz += wy[bq] * (wx[0] * row[ix[0]] + wx[1] * row[ix[1]]);
+    }
+    v += wz[c] * vz;
+  }
   const int64_t p = i + gf.sy * j + gf.sz * k;
   if (ADD) fine[p] += v;
   else fine[p] = v;
@@ -1037,6 +1035,15 @@ __global__ void __launch_bounds__(256) interp_k(const T* __restrict__ coarse, Ge
 // 3D slab versions: z taps are computed from GLOBAL plane indices (zoff) and the
 // global coarse depth ncz; local plane -1 / nz are the ghost planes (filled by the
 // halo exchange before the launch).  On one GPU zoff = 0 and the slab is the grid.
+// Taps are held in registers with a fixed count per axis (4 for restriction, 2 for
+// interpolation; unused taps weigh 0): the tap loops unroll completely.  Same
+// inter-grid stencils of the reference (itkInterGridOperators.h:101-127; restriction
+// taps IGO.h:115-127, interpolation scatter stencils IGO.h:101-113 as gathers):
+//   cell-centred restriction = 1/8,3/8,3/8,1/8 on 2I-1..2I+2 with the fine index
+//   clamped into the grid (which reproduces the one-sided border rows exactly);
+//   vertex-centred = 1/4,1/2,1/4 about 2I, injection at both ends.
+//   cell-centred interpolation = 3/4 c(I) + 1/4 c(I -+ 1), coarse index clamped;
+//   vertex-centred = c(f/2) for even f, (c(f/2) + c(f/2+1)) / 2 for odd f.
 template <typename T, typename A>
 __global__ void __launch_bounds__(256) restrict_slab_k(const T* __restrict__ fine, Geo gf,
                                                        T* __restrict__ coarse, Geo gc, int cx,
@@ -1046,17 +1053,25 @@ __global__ void __launch_bounds__(256) restrict_slab_k(const T* __restrict__ fin
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
   if (I >= gc.nx || J >= gc.ny) return;
   int ix[4], iy[4], iz[4];
-  double wx[4], wy[4], wz[4];
-  const int nxn = restrict_taps(I, gc.nx, cx, ix, wx);
-  const int nyn = restrict_taps(J, gc.ny, cy, iy, wy);
-  const int nzn = restrict_taps(K + gc.zoff, ncz, cz, iz, wz);
+  A wx[4], wy[4], wz[4];
+  rtaps4<A>(I, gc.nx, cx, ix, wx);
+  rtaps4<A>(J, gc.ny, cy, iy, wy);
+  rtaps4<A>(K + gc.zoff, ncz, cz, iz, wz);
   A v = A(0);
-  for (int c = 0; c < nzn; ++c)
-    for (int bq = 0; bq < nyn; ++bq)
-      for (int a = 0; a < nxn; ++a) {
-        const int64_t q = ix[a] + gf.sy * iy[bq] + gf.sz * (int64_t)(iz[c] - fz_shift);
-        v += (A)(wx[a] * wy[bq] * wz[c]) * (A)fine[q];
-      }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const T* pl = fine + gf.sz * (int64_t)(iz[c] - fz_shift);
+    A vz = A(0);
+#pragma unroll
+    for (int bq = 0; bq < 4; ++bq) {
+      const T* row = pl + gf.sy * iy[bq];
+      A vy = A(0);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) vy += wx[a] * (A)row[ix[a]];
+      vz += wy[bq] * vy;
+    }
+    v += wz[c] * vz;
+  }
   coarse[I + gc.sy * J + gc.sz * K] = (T)v;
 }
 
@@ -1069,16 +1084,22 @@ __global__ void __launch_bounds__(256) interp_slab_k(const T* __restrict__ coars
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= gf.nx || j >= gf.ny) return;
   int ix[2], iy[2], iz[2];
-  double wx[2], wy[2], wz[2];
-  const int nxn = interp_taps(i, gc.nx, cx, ix, wx);
-  const int nyn = interp_taps(j, gc.ny, cy, iy, wy);
-  const int nzn = interp_taps(k + gf.zoff, ncz, cz, iz, wz);
+  T wx[2], wy[2], wz[2];
+  itaps2<T>(i, gc.nx, cx, ix, wx);
+  itaps2<T>(j, gc.ny, cy, iy, wy);
+  itaps2<T>(k + gf.zoff, ncz, cz, iz, wz);
   T v = T(0);
-  for (int c = 0; c < nzn; ++c)
-    for (int bq = 0; bq < nyn; ++bq)
-      for (int a = 0; a < nxn; ++a)
-        v += (T)(wx[a] * wy[bq] * wz[c]) *
-             coarse[ix[a] + gc.sy * iy[bq] + gc.sz * (int64_t)(iz[c] - gc.zoff)];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const T* pl = coarse + gc.sz * (int64_t)(iz[c] - gc.zoff);
+    T vz = T(0);
+#pragma unroll
+    for (int bq = 0; bq < 2; ++bq) {
+      const T* row = pl + gc.sy * iy[bq];
+      vz += wy[bq] * (wx[0] * row[ix[0]] + wx[1] * row[ix[1]]);
+    }
+    v += wz[c] * vz;
+  }
   const int64_t p = i + gf.sy * j + gf.sz * k;
   if (ADD) fine[p] += v;
   else fine[p] = v;

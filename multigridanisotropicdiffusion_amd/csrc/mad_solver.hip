@@ -261,10 +261,13 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipMalloc(&L.alloc[a], sizeof(T) * tot));
         HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
       }
-      L.x = L.alloc[0] + margin + L.ghost;
+      // x and t (the fused sweep's ping-pong pair) start xshift elements past the
+      // margin so that a tile region's first column (x = -H) is cache-line aligned
+      const int64_t xs = x_shift();
+      L.x = L.alloc[0] + margin + L.ghost + xs;
       L.b = L.alloc[1] + margin + L.ghost;
       L.r = L.alloc[2] + margin + L.ghost;
-      L.t = L.alloc[3] + margin + L.ghost;
+      L.t = L.alloc[3] + margin + L.ghost + xs;
       // coefficient records, point-interleaved (mad_kernels.hpp, cidx); 3D levels keep
       // GHOST coefficient planes per side: neighbour planes on rank slabs (the fused
       // sweep recomputes colours on them), padding for masked border lanes otherwise
@@ -341,6 +344,15 @@ class Solver final : public SolverBase {
                              std::is_same<T, double>::value, c_->stream);
   }
 
+  // element shift of the x / t arrays (MAD_X_SHIFT, tuning; must stay < margin)
+  static int64_t x_shift() {
+    static const int64_t v = [] {
+      const char* e = std::getenv("MAD_X_SHIFT");
+      return e ? (int64_t)std::max(0, std::min(64, std::atoi(e))) : (int64_t)0;
+    }();
+    return v;
+  }
+
   // rows kept beyond the outermost plane of every level array (see setup)
   // (covers a tile region of up to 40 rows x 256 points hanging over the last plane)
   static int64_t margin_elems(const Geo& g) { return 48 * g.sy + 512; }
@@ -364,14 +376,14 @@ class Solver final : public SolverBase {
   struct FusedCfg {
     int tile = 0, lead = 2, blocks = 2048;
   };
-  // fp32 full tensor: 64x32 tiles of 1024 threads, ~1024 blocks (one per CU slot,
-  // 93 KB LDS); fp64 keeps 64x16/512 (the 64x32 ring would need 186 KB of LDS)
+  // fp32 full tensor: 64x32 tiles of 1024 threads (one block per CU, 93 KB LDS),
+  // ~256 blocks; fp64 keeps 64x16/512 (the 64x32 ring would need 186 KB of LDS)
   static const FusedCfg& fused_cfg() {
     static FusedCfg c = [] {
       FusedCfg f;
       if (sizeof(T) == 4) {
         f.tile = 1;
-        f.blocks = 1024;
+        f.blocks = 256;  // one round, z-chunks of 256 planes at 512^3: least chunk-overlap re-reads
       }
       if (const char* e = std::getenv("MAD_FUSED_TILE")) f.tile = std::atoi(e);
       if (const char* e = std::getenv("MAD_FUSED_LEAD")) f.lead = std::atoi(e);

@@ -68,6 +68,9 @@ def main():
             groups.setdefault(g, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         gmax = max(groups)
         d = groups[gmax]
+        # coarser levels can launch the same grid (z-chunks): keep the level-0 cluster
+        # (durations within 40% of the longest dispatch of that grid)
+        d = [v for v in d if v >= 0.6 * max(d)]
         lvl0 = sum(d) / len(d) / 1e3
         res["trace_avg_us_level0"] = lvl0
         res["trace_level0_calls"] = len(d)

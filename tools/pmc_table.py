@@ -12,7 +12,9 @@ def main():
     p.add_argument("--kernel", default="")
     a = p.parse_args()
     acc = {}
-    for f in sorted(glob.glob(os.path.join(a.root, "*", "*counter_collection.csv"))):
+    files = glob.glob(os.path.join(a.root, "*", "*counter_collection.csv")) + \
+        glob.glob(os.path.join(a.root, "*counter_collection.csv"))
+    for f in sorted(files):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0]
             if a.kernel not in k:
