@@ -17,6 +17,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 
 namespace mad {
@@ -121,6 +122,14 @@ __device__ __forceinline__ void stencil_combine(const Coefs<T>& q, const T* nb, 
   }
   D = T(1) + d;
   S = s;
+}
+
+// r = b - (D u - S), rounded the same way in every residual kernel
+template <typename T>
+__device__ __forceinline__ T resid_value(T b, T D, T u, T S) {
+#pragma clang fp contract(off)
+  const T Du = D * u;
+  return b - (Du - S);
 }
 
 template <int DIM, int KIND>
@@ -276,27 +285,39 @@ __device__ __forceinline__ void coefs_from_raw(const T* raw, const Rat<T>& rat, 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
 }
-template <typename T>
+template <typename T, int AUX = 0>
 __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   if constexpr (sizeof(T) == 4) {
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, AUX));
   } else {
-    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, AUX);
     return __builtin_bit_cast(T, v);
   }
 }
-template <typename T>
+template <typename T, int AUX = 0>
 __device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
   if constexpr (sizeof(T) == 4) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, 0, AUX);
   } else {
     using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, (int)voff, 0, AUX);
   }
 }
 
 // one coefficient record (NCF values of T) at byte offset voff: dword x3 chunks when
 // the record is a multiple of 12 bytes, else x4 chunks + remainder
+// cache policy of the fused sweep's streams (aux bits of the buffer instructions;
+// 2 = nt).  Default policy unless a measurement build overrides them.
+#ifndef MAD_REC_AUX
+#define MAD_REC_AUX 0
+#endif
+#ifndef MAD_U_AUX
+#define MAD_U_AUX 0
+#endif
+#ifndef MAD_ST_AUX
+#define MAD_ST_AUX 0
+#endif
+
 template <typename T, int NCF>
 __device__ __forceinline__ void buf_load_rec(__amdgpu_buffer_rsrc_t r, uint32_t voff, T* out) {
   constexpr int NB = NCF * (int)sizeof(T);
@@ -306,24 +327,24 @@ __device__ __forceinline__ void buf_load_rec(__amdgpu_buffer_rsrc_t r, uint32_t 
   if constexpr (NB % 12 == 0 && NB % 16 != 0) {
 #pragma unroll
     for (int q = 0; q < NW / 3; ++q) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 12 * q, 0);
+      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 12 * q, MAD_REC_AUX);
       w[3 * q] = v[0]; w[3 * q + 1] = v[1]; w[3 * q + 2] = v[2];
     }
   } else {
     int q = 0;
 #pragma unroll
     for (; q + 4 <= NW; q += 4) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 4 * q, 0);
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 4 * q, MAD_REC_AUX);
       w[q] = v[0]; w[q + 1] = v[1]; w[q + 2] = v[2]; w[q + 3] = v[3];
     }
     if constexpr (NW % 4 == 3) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 4 * (NW - 3), 0);
+      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 4 * (NW - 3), MAD_REC_AUX);
       w[NW - 3] = v[0]; w[NW - 2] = v[1]; w[NW - 1] = v[2];
     } else if constexpr (NW % 4 == 2) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 4 * (NW - 2), 0);
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 4 * (NW - 2), MAD_REC_AUX);
       w[NW - 2] = v[0]; w[NW - 1] = v[1];
     } else if constexpr (NW % 4 == 1) {
-      w[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 4 * (NW - 1), 0);
+      w[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 4 * (NW - 1), MAD_REC_AUX);
     }
   }
   __builtin_memcpy(out, w, NB);
@@ -569,7 +590,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
   static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
   extern __shared__ __align__(16) unsigned char fused_smem[];
-  T* lds = reinterpret_cast<T*>(fused_smem);
 
   int bid = blockIdx.x;
   {
@@ -701,7 +721,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     for (int e = 0; e < UPT; ++e) up[e] = T(0);
 #else
 #pragma unroll
-    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src(e), 0u);
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T, MAD_U_AUX>(rs, u_src(e), 0u);
 #endif
   };
   auto put_plane = [&](int m) {
@@ -842,7 +862,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
             const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
             const int gi = rx0 + li, gj = ry0 + lj;
             if (q < TX * TY && gi < nx && gj < ny)
-              buf_store<T>(*reinterpret_cast<const T*>(P + (lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS),
+              buf_store<T, MAD_ST_AUX>(*reinterpret_cast<const T*>(P + (lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS),
                            ro, (uint32_t)(gj * sy + gi) * TS);
           }
         }
@@ -905,7 +925,7 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
     const int64_t p = i + g.sy * j + g.sz * k;
     T D, S;
     stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
-    const T rv = b[p] - (D * u[p] - S);
+    const T rv = resid_value(b[p], D, u[p], S);
     r[p] = rv;
     sq = (double)rv * (double)rv;
   }
@@ -913,6 +933,132 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
     const double s = block_sum<256>(sq);
     if (threadIdx.x == 0 && threadIdx.y == 0)
       part[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = s;
+  }
+}
+
+// residual r = b - A u, 3D, z-marching (the residual_k arithmetic, bit-identical):
+// each workgroup owns a TX x TY column of one z-chunk, keeps a 4-slot LDS ring of u
+// planes over the tile + 1 (mirror images of the domain faces stored in the ring, as
+// in gs_fused3_k), reads each point's coefficient record with wide buffer loads one
+// step ahead, and writes r (and optionally fp64 |r|^2 partials per workgroup).
+// One barrier per plane.  Needs the GHOST x/b planes and coefficient padding planes
+// of LevelData (masked lanes read inside them).
+template <typename T, int KIND, int TX, int TY>
+__global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const T* __restrict__ b,
+                                                    T* __restrict__ r, const T* __restrict__ cf,
+                                                    Geo g, Rat<T> rat, int zc, int ntx,
+                                                    double* __restrict__ part) {
+  constexpr int NT = TX * TY;
+  constexpr int RX = TX + 2, RY = TY + 2, PL = RX * RY;
+  constexpr int UPT = (PL + NT - 1) / NT;
+  constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr uint32_t TS = sizeof(T);
+  __shared__ T ring[4 * PL];
+  const int tiles_per_plane = ntx * ((g.ny + TY - 1) / TY);
+  const int chunk = blockIdx.x / tiles_per_plane;
+  const int tile = blockIdx.x - chunk * tiles_per_plane;
+  const int tyi = tile / ntx, txi = tile - (tile / ntx) * ntx;
+  const int x0 = txi * TX, y0 = tyi * TY;  // x0 even
+  const int tid = threadIdx.x;
+  const int tx = tid % TX, ty = tid / TX;
+  const int nx = g.nx, ny = g.ny, sy = (int)g.sy, hx0 = g.hx0;
+  const int64_t sz = g.sz;
+  const int z0 = chunk * zc, z1 = min(z0 + zc, g.nz);
+  const int zlo = g.zlo_ghost ? -1 : 0, zhi = g.zhi_ghost ? g.nz + 1 : g.nz;
+  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
+  // region element e of this thread: LDS index and mirrored in-plane source offset
+  int u_dst[UPT];
+  uint32_t u_src[UPT];
+#pragma unroll
+  for (int e = 0; e < UPT; ++e) {
+    const int q = tid + e * NT;
+    const int lj = q / RX, li = q - (q / RX) * RX;
+    u_dst[e] = q < PL ? q : -1;
+    u_src[e] = (uint32_t)(mirror(y0 - 1 + lj, ny) * sy + mirror(x0 - 1 + li, nx)) * TS;
+  }
+  const int i = x0 + tx, j = y0 + ty;
+  const bool ok = i < nx && j < ny;
+  const uint32_t rec_off = ok ? (uint32_t)(ty * sy + (tx & 1) * hx0 + (tx >> 1)) * (TS * NCF) : 0u;
+  const uint32_t pt_off = ok ? (uint32_t)(ty * sy + tx) * TS : 0u;
+  const int64_t rbase = (int64_t)y0 * sy + (x0 >> 1), pbase = (int64_t)y0 * sy + x0;
+  const int il = (ty + 1) * RX + (tx + 1);
+  constexpr int oyp = RX, oym = -RX;  // x/y mirror images live in the ring
+
+  T up[UPT];
+  T raw[NCF];
+  T bv;
+  auto load_plane = [&](int m) {
+    m = min(max(m, zlo), zhi - 1);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src[e], 0u);
+  };
+  auto put_plane = [&](int m) {
+    T* P = ring + (m & 3) * PL;
+#pragma unroll
+    for (int e = 0; e < UPT; ++e)
+      if (e < UPT - 1 || u_dst[e] >= 0) P[u_dst[e]] = up[e];
+  };
+  auto load_pt = [&](int m) {
+    m = min(max(m, 0), g.nz - 1);
+    buf_load_rec<T, NCF>(buf_rsrc(cf + ((int64_t)m * sz + rbase) * NCF), rec_off, raw);
+    bv = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + pbase), pt_off, 0u);
+  };
+
+  // prologue: planes z0-1, z0 in the ring, z0+1 in registers, point data of z0
+  if (z0 - 1 >= zlo) {
+    load_plane(z0 - 1);
+    put_plane(z0 - 1);
+  }
+  load_plane(z0);
+  put_plane(z0);
+  load_plane(z0 + 1);
+  load_pt(z0);
+  double sq = 0.0;
+  for (int m = z0; m < z1; ++m) {
+    if (m + 1 < zhi) put_plane(m + 1);
+    load_plane(m + 2);
+    __syncthreads();
+    const int zm = (m == 0 && !g.zlo_ghost) ? m + 1 : m - 1;
+    const int zp = (m == g.nz - 1 && !g.zhi_ghost) ? m - 1 : m + 1;
+    const T* P0 = ring + (m & 3) * PL + il;
+    const T* Pm = ring + (zm & 3) * PL + il;
+    const T* Pp = ring + (zp & 3) * PL + il;
+    T nb[18];
+    nb[0] = P0[1];
+    nb[1] = P0[-1];
+    nb[2] = P0[oyp];
+    nb[3] = P0[oym];
+    nb[4] = Pp[0];
+    nb[5] = Pm[0];
+    if (KIND == KFULL) {
+      nb[6] = P0[1 + oyp];
+      nb[7] = P0[1 + oym];
+      nb[8] = P0[-1 + oyp];
+      nb[9] = P0[-1 + oym];
+      nb[10] = Pp[1];
+      nb[11] = Pm[1];
+      nb[12] = Pp[-1];
+      nb[13] = Pm[-1];
+      nb[14] = Pp[oyp];
+      nb[15] = Pm[oyp];
+      nb[16] = Pp[oym];
+      nb[17] = Pm[oym];
+    }
+    Coefs<T> q;
+    coefs_from_raw<T, 3, KIND>(raw, rat, q);
+    T D, S;
+    stencil_combine<T, 3, KIND>(q, nb, D, S);
+    const T rv = resid_value(bv, D, P0[0], S);
+    load_pt(m + 1);
+    if (ok) {
+      buf_store<T>(rv, buf_rsrc(r + (int64_t)m * sz + pbase), pt_off);
+      sq += (double)rv * (double)rv;
+    }
+  }
+  if (part) {
+    const double s = block_sum<NT>(sq);
+    if (tid == 0) part[blockIdx.x] = s;
   }
 }
 
@@ -974,6 +1120,7 @@ template <typename T, typename A, int DIM>
 __global__ void __launch_bounds__(256) restrict_k(const T* __restrict__ fine, Geo gf,
                                                   T* __restrict__ coarse, Geo gc, int cx, int cy,
                                                   int cz, int fz_shift) {
+#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   const int K = (DIM == 3) ? (int)blockIdx.z : 0;
   const int J = blockIdx.y * blockDim.y + threadIdx.y;
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
@@ -993,10 +1140,10 @@ __global__ void __launch_bounds__(256) restrict_k(const T* __restrict__ fine, Ge
       const T* row = pl + gf.sy * iy[bq];
       A vy = A(0);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) vy += wx[a] * (A)row[ix[a]];
-      vz += wy[bq] * vy;
+      for (int a = 0; a < 4; ++a) vy = fma(wx[a], (A)row[ix[a]], vy);
+      vz = fma(wy[bq], vy, vz);
     }
-    v += wz[c] * vz;
+    v = fma(wz[c], vz, v);
   }
   coarse[I + gc.sy * J + gc.sz * K] = (T)v;
 }
@@ -1006,6 +1153,7 @@ template <typename T, int DIM, int ADD>
 __global__ void __launch_bounds__(256) interp_k(const T* __restrict__ coarse, Geo gc,
                                                 T* __restrict__ fine, Geo gf, int cx, int cy,
                                                 int cz) {
+#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   const int k = (DIM == 3) ? (int)blockIdx.z : 0;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1023,9 +1171,9 @@ __global__ void __launch_bounds__(256) interp_k(const T* __restrict__ coarse, Ge
 #pragma unroll
     for (int bq = 0; bq < 2; ++bq) {
       const T* row = pl + gc.sy * iy[bq];
-      vz += wy[bq] * (wx[0] * row[ix[0]] + wx[1] * row[ix[1]]);
+      vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
     }
-    v += wz[c] * vz;
+    v = fma(wz[c], vz, v);
   }
   const int64_t p = i + gf.sy * j + gf.sz * k;
   if (ADD) fine[p] += v;
@@ -1048,6 +1196,7 @@ template <typename T, typename A>
 __global__ void __launch_bounds__(256) restrict_slab_k(const T* __restrict__ fine, Geo gf,
                                                        T* __restrict__ coarse, Geo gc, int cx,
                                                        int cy, int cz, int fz_shift, int ncz) {
+#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   const int K = blockIdx.z;
   const int J = blockIdx.y * blockDim.y + threadIdx.y;
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1067,10 +1216,10 @@ __global__ void __launch_bounds__(256) restrict_slab_k(const T* __restrict__ fin
       const T* row = pl + gf.sy * iy[bq];
       A vy = A(0);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) vy += wx[a] * (A)row[ix[a]];
-      vz += wy[bq] * vy;
+      for (int a = 0; a < 4; ++a) vy = fma(wx[a], (A)row[ix[a]], vy);
+      vz = fma(wy[bq], vy, vz);
     }
-    v += wz[c] * vz;
+    v = fma(wz[c], vz, v);
   }
   coarse[I + gc.sy * J + gc.sz * K] = (T)v;
 }
@@ -1079,6 +1228,7 @@ template <typename T, int ADD>
 __global__ void __launch_bounds__(256) interp_slab_k(const T* __restrict__ coarse, Geo gc,
                                                      T* __restrict__ fine, Geo gf, int cx, int cy,
                                                      int cz, int ncz) {
+#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   const int k = blockIdx.z;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1096,13 +1246,166 @@ __global__ void __launch_bounds__(256) interp_slab_k(const T* __restrict__ coars
 #pragma unroll
     for (int bq = 0; bq < 2; ++bq) {
       const T* row = pl + gc.sy * iy[bq];
-      vz += wy[bq] * (wx[0] * row[ix[0]] + wx[1] * row[ix[1]]);
+      vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
     }
-    v += wz[c] * vz;
+    v = fma(wz[c], vz, v);
   }
   const int64_t p = i + gf.sy * j + gf.sz * k;
   if (ADD) fine[p] += v;
   else fine[p] = v;
+}
+
+// z-marching 3D transfers (same taps and summation order as restrict_slab_k /
+// interp_slab_k, so results are bit-identical): each workgroup owns a tile column,
+// stages one plane at a time in LDS (coalesced loads, each fine / coarse value read
+// once from HBM), and carries the z dimension in registers.
+//
+// restrict3_k: coarse tile CX x CY (one thread per coarse point), coarse planes
+// [K0, K1).  Marches the fine planes the chunk needs in order: each fine plane is
+// staged in LDS once (the next one already in registers), its x-y restricted value
+// goes into a 4-entry register window, and a coarse plane is emitted once its last
+// fine tap has been seen.
+template <typename T, typename A, int CX, int CY>
+__global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fine, Geo gf,
+                                                       T* __restrict__ coarse, Geo gc, int cx,
+                                                       int cy, int cz, int fz_shift, int ncz,
+                                                       int kc, int ntx) {
+#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
+  constexpr int NT = CX * CY;
+  constexpr int FX = 2 * CX + 2, FY = 2 * CY + 2, FP = FX * FY;
+  constexpr int EPT = (FP + NT - 1) / NT;
+  __shared__ T tile[FP];
+  const int tiles = ntx * ((gc.ny + CY - 1) / CY);
+  const int chunk = blockIdx.x / tiles;
+  const int t = blockIdx.x - chunk * tiles;
+  const int tyi = t / ntx, txi = t - (t / ntx) * ntx;
+  const int I0 = txi * CX, J0 = tyi * CY;
+  const int tid = threadIdx.x;
+  const int I = I0 + tid % CX, J = J0 + tid / CX;
+  const bool ok = I < gc.nx && J < gc.ny;
+  const int fx0 = 2 * I0 - 1, fy0 = 2 * J0 - 1;  // tile origin in fine indices
+  int ix[4], iy[4];
+  A wx[4], wy[4];
+  rtaps4<A>(min(I, gc.nx - 1), gc.nx, cx, ix, wx);
+  rtaps4<A>(min(J, gc.ny - 1), gc.ny, cy, iy, wy);
+  // this thread's tile elements: clamped in-plane source offsets
+  int src_off[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = min(tid + q * NT, FP - 1);
+    const int ly = e / FX, lx = e - (e / FX) * FX;
+    src_off[q] = min(max(fy0 + ly, 0), gf.ny - 1) * (int)gf.sy + min(max(fx0 + lx, 0), gf.nx - 1);
+  }
+  const int K0 = chunk * kc, K1 = min(K0 + kc, gc.nz);
+  int iz[4];
+  A wz[4];
+  rtaps4<A>(K0 + gc.zoff, ncz, cz, iz, wz);
+  const int f_lo = iz[0];
+  rtaps4<A>(K1 - 1 + gc.zoff, ncz, cz, iz, wz);
+  const int f_hi = max(max(iz[0], iz[1]), max(iz[2], iz[3]));
+  T reg[EPT];
+  auto fetch = [&](int f) {
+    const T* src = fine + gf.sz * (int64_t)(f - fz_shift);
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) reg[q] = src[src_off[q]];
+  };
+  A win[4];
+  int K = K0;
+  rtaps4<A>(K + gc.zoff, ncz, cz, iz, wz);
+  fetch(f_lo);
+  for (int f = f_lo; f <= f_hi; ++f) {
+    __syncthreads();  // the previous plane's reads of `tile` are done
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+      if (tid + q * NT < FP) tile[tid + q * NT] = reg[q];
+    if (f < f_hi) fetch(f + 1);
+    __syncthreads();
+    A vz = A(0);
+#pragma unroll
+    for (int bq = 0; bq < 4; ++bq) {
+      const T* row = tile + (iy[bq] - fy0) * FX - fx0;
+      A vy = A(0);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) vy = fma(wx[a], (A)row[ix[a]], vy);
+      vz = fma(wy[bq], vy, vz);
+    }
+    win[f & 3] = vz;
+    // emit every coarse plane whose last tap is f (uniform)
+    while (K < K1 && max(max(iz[0], iz[1]), max(iz[2], iz[3])) == f) {
+      A v = A(0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v = fma(wz[c], win[iz[c] & 3], v);
+      if (ok) coarse[I + gc.sy * J + gc.sz * (int64_t)K] = (T)v;
+      ++K;
+      if (K < K1) rtaps4<A>(K + gc.zoff, ncz, cz, iz, wz);
+    }
+  }
+}
+
+// interp3_k: fine tile TX x TY (one thread per fine point), fine planes [k0, k1);
+// coarse planes staged in a 4-slot LDS ring one fine plane ahead; the fine value of
+// the next plane is prefetched into a register.
+template <typename T, int ADD, int TX, int TY>
+__global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coarse, Geo gc,
+                                                     T* __restrict__ fine, Geo gf, int cx, int cy,
+                                                     int cz, int ncz, int kc, int ntx) {
+#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
+  constexpr int NT = TX * TY;
+  constexpr int CXW = TX / 2 + 2, CYW = TY / 2 + 2, CP = CXW * CYW;
+  __shared__ T ring[4 * CP];
+  const int tiles = ntx * ((gf.ny + TY - 1) / TY);
+  const int chunk = blockIdx.x / tiles;
+  const int t = blockIdx.x - chunk * tiles;
+  const int tyi = t / ntx, txi = t - (t / ntx) * ntx;
+  const int i0 = txi * TX, j0 = tyi * TY;
+  const int tid = threadIdx.x;
+  const int i = i0 + tid % TX, j = j0 + tid / TX;
+  const bool ok = i < gf.nx && j < gf.ny;
+  const int cx0 = i0 / 2 - 1, cy0 = j0 / 2 - 1;  // coarse tile origin
+  int ix[2], iy[2];
+  T wx[2], wy[2];
+  itaps2<T>(min(i, gf.nx - 1), gc.nx, cx, ix, wx);
+  itaps2<T>(min(j, gf.ny - 1), gc.ny, cy, iy, wy);
+  const int ci = tid < CP ? tid : CP - 1;  // one ring element per thread (CP <= NT)
+  const int c_off = min(max(cy0 + ci / CXW, 0), gc.ny - 1) * (int)gc.sy +
+                    min(max(cx0 + ci % CXW, 0), gc.nx - 1);
+  const int k0 = chunk * kc, k1 = min(k0 + kc, gf.nz);
+  const int64_t pxy = (int64_t)j * gf.sy + i;
+  int last = INT_MIN;  // largest coarse plane (global) in the ring
+  T xn = (ADD && ok && k0 < k1) ? fine[pxy + gf.sz * (int64_t)k0] : T(0);
+  for (int k = k0; k < k1; ++k) {
+    int iz[2], jz[2];
+    T wz[2], vz2[2];
+    itaps2<T>(k + gf.zoff, ncz, cz, iz, wz);
+    itaps2<T>(min(k + 1, gf.nz - 1) + gf.zoff, ncz, cz, jz, vz2);
+    // coarse planes min(iz)..max(jz) not yet in the ring (even fine planes have taps
+    // {K, K-1}: not ordered, so ranges)
+    const int need_hi = max(max(iz[0], iz[1]), max(jz[0], jz[1]));
+    for (int c = max(min(iz[0], iz[1]), last + 1); c <= need_hi; ++c)
+      if (tid < CP) ring[(c & 3) * CP + tid] = coarse[gc.sz * (int64_t)(c - gc.zoff) + c_off];
+    last = max(last, need_hi);
+    const T xc = xn;
+    if (ADD && ok && k + 1 < k1) xn = fine[pxy + gf.sz * (int64_t)(k + 1)];
+    __syncthreads();
+    T v = T(0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const T* pl = ring + (iz[c] & 3) * CP - cx0;
+      T vz = T(0);
+#pragma unroll
+      for (int bq = 0; bq < 2; ++bq) {
+        const T* row = pl + (iy[bq] - cy0) * CXW;
+        vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
+      }
+      v = fma(wz[c], vz, v);
+    }
+    if (ok) {
+      const int64_t p = pxy + gf.sz * (int64_t)k;
+      if (ADD) fine[p] = xc + v;
+      else fine[p] = v;
+    }
+    __syncthreads();  // ring slots are reused two planes later
+  }
 }
 
 // ---------------------------------------------------------------------------

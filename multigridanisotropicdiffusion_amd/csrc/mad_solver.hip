@@ -283,6 +283,7 @@ class Solver final : public SolverBase {
     }
     part_need = std::max<int64_t>(part_need, 4096);
     HIP_CHECK(hipMalloc(&part_, sizeof(double) * part_need));
+    part_cap_ = part_need;
     HIP_CHECK(hipMalloc(&scal_, sizeof(double) * 4));
     HIP_CHECK(hipHostMalloc(&hscal_, sizeof(double) * 4, hipHostMallocDefault));
     build_operators();
@@ -342,6 +343,15 @@ class Solver final : public SolverBase {
     LevelData<T>& L = lv_[l];
     c_->comm.exchange_planes(a, L.g.sz, L.g.nz, depth, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
                              std::is_same<T, double>::value, c_->stream);
+  }
+
+  // target grid size of the z-marching transfer kernels (MAD_XFER_BLOCKS, tuning)
+  static int xfer_blocks() {
+    static const int v = [] {
+      const char* e = std::getenv("MAD_XFER_BLOCKS");
+      return e ? std::max(1, std::atoi(e)) : 1024;
+    }();
+    return v;
   }
 
   // element shift of the x / t arrays (MAD_X_SHIFT, tuning; must stay < margin)
@@ -551,14 +561,35 @@ class Solver final : public SolverBase {
   double residual(int l, bool want_norm) override {
     LevelData<T>& L = lv_[l];
     halo(l, L.x);
-    dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
-    dispatch(c_->dim, c_->kind, [&](auto D, auto K) {
-      hipLaunchKernelGGL((residual_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, L.x, L.b, L.r,
-                         L.cf, L.g, L.rat, want_norm ? part_ : nullptr);
-    });
+    int64_t nparts = 0;
+    if (c_->dim == 3 && L.g.nx >= 16 && L.g.ny >= 16) {
+      // z-marching residual (resid3_k): 64x16 columns, chunks sized for ~1024 blocks
+      constexpr int TX = 64, TY = 16;
+      const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
+      int chunks = std::max(1, std::min((1024 + ntx * nty - 1) / (ntx * nty), L.g.nz / 8));
+      const int zc = (L.g.nz + chunks - 1) / chunks;
+      chunks = (L.g.nz + zc - 1) / zc;
+      nparts = (int64_t)ntx * nty * chunks;
+      REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
+      auto go = [&](auto K) {
+        hipLaunchKernelGGL((resid3_k<T, decltype(K)::value, TX, TY>), dim3((unsigned)nparts),
+                           dim3(TX * TY), 0, c_->stream, L.x, L.b, L.r, L.cf, L.g, L.rat, zc, ntx,
+                           want_norm ? part_ : nullptr);
+      };
+      if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
+      else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
+      else go(std::integral_constant<int, KISO>{});
+    } else {
+      dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
+      nparts = (int64_t)gr.x * gr.y * gr.z;
+      dispatch(c_->dim, c_->kind, [&](auto D, auto K) {
+        hipLaunchKernelGGL((residual_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, L.x, L.b,
+                           L.r, L.cf, L.g, L.rat, want_norm ? part_ : nullptr);
+      });
+    }
     HIP_CHECK(hipGetLastError());
     if (!want_norm) return 0.0;
-    return std::sqrt(finish_norm2((int64_t)gr.x * gr.y * gr.z, c_->geom[l].distributed));
+    return std::sqrt(finish_norm2(nparts, c_->geom[l].distributed));
   }
 
   double norm(int l, int which) override {
@@ -584,8 +615,16 @@ class Solver final : public SolverBase {
     Geo gc = C.g;
     if (c_->dim == 3) gc.zoff = C.g.zoff;
     if (c_->dim == 3) {
-      hipLaunchKernelGGL((restrict_slab_k<T, T>), gr, BLK, 0, c_->stream, fine, F.g, coarse, gc,
-                         C.cent[0], C.cent[1], C.cent[2], fz_shift, (int)c_->geom[l + 1].n[2]);
+      // z-marching (restrict3_k): 32x8 coarse columns, ~1024 blocks
+      constexpr int CX = 32, CY = 8;
+      const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
+      int chunks = std::max(1, std::min((xfer_blocks() + ntx * nty - 1) / (ntx * nty), C.g.nz / 4));
+      const int kc = (C.g.nz + chunks - 1) / chunks;
+      chunks = (C.g.nz + kc - 1) / kc;
+      hipLaunchKernelGGL((restrict3_k<T, T, CX, CY>), dim3((unsigned)(ntx * nty * chunks)),
+                         dim3(CX * CY), 0, c_->stream, fine, F.g, coarse, gc, C.cent[0], C.cent[1],
+                         C.cent[2], fz_shift, (int)c_->geom[l + 1].n[2], kc, ntx);
+      (void)gr;
     } else {
       hipLaunchKernelGGL((restrict_k<T, T, 2>), gr, BLK, 0, c_->stream, fine, F.g, coarse, C.g,
                          C.cent[0], C.cent[1], C.cent[2], 0);
@@ -600,12 +639,7 @@ class Solver final : public SolverBase {
     halo(l + 1, C.x);
     dim3 gr = grid_for(F.g.nx, F.g.ny, F.g.nz, BLK);
     if (c_->dim == 3) {
-      if (add)
-        hipLaunchKernelGGL((interp_slab_k<T, 1>), gr, BLK, 0, c_->stream, C.x, C.g, F.x, F.g,
-                           C.cent[0], C.cent[1], C.cent[2], (int)c_->geom[l + 1].n[2]);
-      else
-        hipLaunchKernelGGL((interp_slab_k<T, 0>), gr, BLK, 0, c_->stream, C.x, C.g, F.x, F.g,
-                           C.cent[0], C.cent[1], C.cent[2], (int)c_->geom[l + 1].n[2]);
+      launch_interp3(l, add);
     } else {
       if (add)
         hipLaunchKernelGGL((interp_k<T, 2, 1>), gr, BLK, 0, c_->stream, C.x, C.g, F.x, F.g,
@@ -972,6 +1006,7 @@ class Solver final : public SolverBase {
  private:
   mad_ctx* c_ = nullptr;
   std::vector<LevelData<T>> lv_;
+  int64_t part_cap_ = 0;             // entries of part_
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
   bool vgraph_failed_ = false;
   int ncoef_ = 0;
@@ -1254,16 +1289,28 @@ class Solver final : public SolverBase {
 
   // fine slab (distributed) from the replicated coarse level
   void interp_from_replicated(int l, bool add) {
+    launch_interp3(l, add);
+    HIP_CHECK(hipGetLastError());
+  }
+
+  // x[l] (+)= P x[l+1], 3D, z-marching (interp3_k): 64x16 fine columns, ~1024 blocks.
+  // The coarse level may be a slab (ghost planes exchanged) or replicated (zoff 0).
+  void launch_interp3(int l, bool add) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
-    dim3 gr = grid_for(F.g.nx, F.g.ny, F.g.nz, BLK);
+    constexpr int TX = 64, TY = 16;
+    const int ntx = (F.g.nx + TX - 1) / TX, nty = (F.g.ny + TY - 1) / TY;
+    int chunks = std::max(1, std::min((xfer_blocks() + ntx * nty - 1) / (ntx * nty), F.g.nz / 4));
+    const int kc = (F.g.nz + chunks - 1) / chunks;
+    chunks = (F.g.nz + kc - 1) / kc;
+    const unsigned nb = (unsigned)(ntx * nty * chunks);
+    const int ncz = (int)c_->geom[l + 1].n[2];
     if (add)
-      hipLaunchKernelGGL((interp_slab_k<T, 1>), gr, BLK, 0, c_->stream, C.x, C.g, F.x, F.g,
-                         C.cent[0], C.cent[1], C.cent[2], (int)c_->geom[l + 1].n[2]);
+      hipLaunchKernelGGL((interp3_k<T, 1, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
+                         C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx);
     else
-      hipLaunchKernelGGL((interp_slab_k<T, 0>), gr, BLK, 0, c_->stream, C.x, C.g, F.x, F.g,
-                         C.cent[0], C.cent[1], C.cent[2], (int)c_->geom[l + 1].n[2]);
-    HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((interp3_k<T, 0, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
+                         C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx);
   }
 };
 
