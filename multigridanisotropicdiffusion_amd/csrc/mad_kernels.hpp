@@ -59,6 +59,8 @@ struct Geo {
   int hx0;              // (nx + 1) / 2: start of the odd-x half of a coefficient row
   int64_t sy, sz;       // strides
   int64_t N;            // nx*ny*nz (owned points)
+  int rs;               // coefficient record stride (ncoef, or ncoef + 1 when the record
+                        // also carries the rhs b: level 0, see LevelData::brec)
 };
 
 // coefficient record index of point (i, j, k): element cidx * NCF + field
@@ -82,10 +84,10 @@ template <typename T, int DIM, int KIND>
 __device__ __forceinline__ void coefs_from_raw(const T* raw, const Rat<T>& rat, Coefs<T>& q);
 
 template <typename T, int DIM, int KIND>
-__device__ __forceinline__ void load_coefs(const T* __restrict__ cf, int64_t c, const Rat<T>& rat,
-                                           Coefs<T>& q) {
+__device__ __forceinline__ void load_coefs(const T* __restrict__ cf, int64_t c, int rs,
+                                           const Rat<T>& rat, Coefs<T>& q) {
   constexpr int NCF = CoefLayout<DIM, KIND>::N;
-  const T* rec = cf + c * NCF;
+  const T* rec = cf + c * rs;
   T raw[NCF];
 #pragma unroll
   for (int a = 0; a < NCF; ++a) raw[a] = rec[a];
@@ -179,7 +181,7 @@ __device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* 
                                               const Geo& g, const Rat<T>& rat, int i, int j,
                                               int k, int64_t p, T& D, T& S) {
   Coefs<T> q;
-  load_coefs<T, DIM, KIND>(cf, cidx(g, i, j, k), rat, q);
+  load_coefs<T, DIM, KIND>(cf, cidx(g, i, j, k), g.rs, rat, q);
   T nb[18];
   gather_nb<T, DIM, KIND>(u, g, i, j, k, p, nb);
   stencil_combine<T, DIM, KIND>(q, nb, D, S);
@@ -470,10 +472,10 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
     int li, lj;
     if (stage_on(c, m) && locate(c, m, li, lj)) {
       const int gi = rx0 + li, gj = ry0 + lj;
-      const T* cp = cf + (int64_t)m * sz * NCF;
+      const T* cp = cf + (int64_t)m * sz * g.rs;
       const int co = gj * sy + ((gi & 1) ? g.hx0 + (gi >> 1) : (gi >> 1));
 #pragma unroll
-      for (int a = 0; a < NCF; ++a) raw[c][a] = cp[(int64_t)co * NCF + a];
+      for (int a = 0; a < NCF; ++a) raw[c][a] = cp[(int64_t)co * g.rs + a];
       bv[c] = b[(int64_t)m * sz + gj * sy + gi];
     }
   };
@@ -575,7 +577,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
 // Needs: coefficient fields with >= 1 padding plane below and above every field
 // (LevelData::cf, GHOST planes) and x/b arrays with their GHOST planes; nx, ny >= 3.
 // LDS: dynamic, NP * PLANE * sizeof(T) bytes.
-template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2>
+template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty) {
@@ -586,6 +588,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   constexpr int UPT = (RX * RY + NT - 1) / NT;
   constexpr int OPT = (TX * TY + NT - 1) / NT;
   constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr int RS = NCF + (BREC ? 1 : 0);  // record stride; BREC: b is the record's last value
   constexpr uint32_t TS = sizeof(T);
   static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
   static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
@@ -680,7 +683,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       omask |= (uint32_t)(li & 1) << (c * 2 + PM);
       if (PM < NPM) {
         pl[c][PM] = (uint32_t)(lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS;
-        pg[c][PM] = (uint32_t)(lj * sy + (li & 1) * hx0 + (li >> 1)) * (TS * NCF);
+        pg[c][PM] = (uint32_t)(lj * sy + (li & 1) * hx0 + (li >> 1)) * (TS * RS);
         pb[c][PM] = (uint32_t)(lj * sy + li) * TS;
       }
     }
@@ -710,7 +713,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   unsigned char* lbytes = fused_smem;
 
   T up[UPT];
-  T raw[NC][NCF];
+  T raw[NC][RS];
   T bv[NC];
   auto load_plane = [&](int m) {
     m = min(max(m, zlo), zhi - 1);
@@ -739,13 +742,15 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     const int m = min(max(k - c, zlo), zhi - 1);
     {
       const PD d = pdelta(c, PM);
-      buf_load_rec<T, NCF>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * NCF), pg[c][PM % NPM],
-                           raw[c]);
+      buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * RS), pg[c][PM % NPM],
+                          raw[c]);
+      if constexpr (!BREC) {
 #ifdef MAD_PROBE_NO_B  // measurement builds only (tools/probe_builds.sh): drop the rhs stream
-      bv[c] = T(0);
+        bv[c] = T(0);
 #else
-      bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
+        bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
 #endif
+      }
     }
   };
   auto stage = [&](int c, int k, int PM) {
@@ -792,7 +797,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     coefs_from_raw<T, 3, KIND>(raw[c], rat, q);
     T D, S;
     stencil_combine<T, 3, KIND>(q, nb, D, S);
-    const T v = (bv[c] + S) / D;
+    const T v = ((BREC ? raw[c][NCF] : bv[c]) + S) / D;
     const int bit = c * 2 + PM;
     if (interior) {
       if (NC == 2 || FG::rows(c) * FG::cols(c) < NT) {
@@ -943,7 +948,7 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
 // step ahead, and writes r (and optionally fp64 |r|^2 partials per workgroup).
 // One barrier per plane.  Needs the GHOST x/b planes and coefficient padding planes
 // of LevelData (masked lanes read inside them).
-template <typename T, int KIND, int TX, int TY>
+template <typename T, int KIND, int TX, int TY, bool BREC = false>
 __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const T* __restrict__ b,
                                                     T* __restrict__ r, const T* __restrict__ cf,
                                                     Geo g, Rat<T> rat, int zc, int ntx,
@@ -952,6 +957,7 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
   constexpr int RX = TX + 2, RY = TY + 2, PL = RX * RY;
   constexpr int UPT = (PL + NT - 1) / NT;
   constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr int RS = NCF + (BREC ? 1 : 0);  // record stride; BREC: b is the record's last value
   constexpr uint32_t TS = sizeof(T);
   __shared__ T ring[4 * PL];
   const int tiles_per_plane = ntx * ((g.ny + TY - 1) / TY);
@@ -978,15 +984,15 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
   }
   const int i = x0 + tx, j = y0 + ty;
   const bool ok = i < nx && j < ny;
-  const uint32_t rec_off = ok ? (uint32_t)(ty * sy + (tx & 1) * hx0 + (tx >> 1)) * (TS * NCF) : 0u;
+  const uint32_t rec_off = ok ? (uint32_t)(ty * sy + (tx & 1) * hx0 + (tx >> 1)) * (TS * RS) : 0u;
   const uint32_t pt_off = ok ? (uint32_t)(ty * sy + tx) * TS : 0u;
   const int64_t rbase = (int64_t)y0 * sy + (x0 >> 1), pbase = (int64_t)y0 * sy + x0;
   const int il = (ty + 1) * RX + (tx + 1);
   constexpr int oyp = RX, oym = -RX;  // x/y mirror images live in the ring
 
   T up[UPT];
-  T raw[NCF];
-  T bv;
+  T raw[RS];
+  T bv = T(0);
   auto load_plane = [&](int m) {
     m = min(max(m, zlo), zhi - 1);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
@@ -1001,8 +1007,8 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
   };
   auto load_pt = [&](int m) {
     m = min(max(m, 0), g.nz - 1);
-    buf_load_rec<T, NCF>(buf_rsrc(cf + ((int64_t)m * sz + rbase) * NCF), rec_off, raw);
-    bv = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + pbase), pt_off, 0u);
+    buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + rbase) * RS), rec_off, raw);
+    if constexpr (!BREC) bv = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + pbase), pt_off, 0u);
   };
 
   // prologue: planes z0-1, z0 in the ring, z0+1 in registers, point data of z0
@@ -1049,7 +1055,7 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
     coefs_from_raw<T, 3, KIND>(raw, rat, q);
     T D, S;
     stencil_combine<T, 3, KIND>(q, nb, D, S);
-    const T rv = resid_value(bv, D, P0[0], S);
+    const T rv = resid_value(BREC ? raw[NCF] : bv, D, P0[0], S);
     load_pt(m + 1);
     if (ok) {
       buf_store<T>(rv, buf_rsrc(r + (int64_t)m * sz + pbase), pt_off);
@@ -1408,6 +1414,18 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
   }
 }
 
+// copy the dense rhs into the b slot (index ncf) of the coefficient records of local
+// planes [p0, p1) (ghost planes included on rank slabs): LevelData::brec levels
+template <typename T>
+__global__ void __launch_bounds__(256) brec_scatter_k(const T* __restrict__ b, T* __restrict__ cf,
+                                                      Geo g, int ncf, int p0) {
+  const int k = p0 + (int)blockIdx.z;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.nx || j >= g.ny) return;
+  cf[cidx(g, i, j, k) * g.rs + ncf] = b[i + g.sy * j + g.sz * (int64_t)k];
+}
+
 // ---------------------------------------------------------------------------
 // coarsest-grid solve x = A^-1 b with the precomputed fp64 inverse: one wave per row
 template <typename T>
@@ -1500,7 +1518,7 @@ __device__ __forceinline__ double delta_f(const double* __restrict__ f, int64_t 
 template <typename T, int DIM, int KIND>
 __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M, int nx, int ny,
                                                     int nz, double hx, double hy, double hz,
-                                                    double dt, T* __restrict__ cf) {
+                                                    double dt, T* __restrict__ cf, int rs) {
   using L = CoefLayout<DIM, KIND>;
   const int k = (DIM == 3) ? (int)blockIdx.z : 0;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
@@ -1509,7 +1527,7 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
   const int64_t n = (int64_t)nx * ny * nz;
   const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
   // output record in the point-interleaved, x-parity-split coefficient layout (cidx)
-  const int64_t o = ((int64_t)nx * (j + (int64_t)ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * L::N;
+  const int64_t o = ((int64_t)nx * (j + (int64_t)ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * rs;
   const double h[3] = {hx, hy, hz};
   const int nn[3] = {nx, ny, nz};
   const int id[3] = {i, j, k};

@@ -220,6 +220,12 @@ struct LevelData {
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
+  // brec: the coefficient records also carry b (record stride g.rs = ncoef + 1), so the
+  // sweep / residual read it with the record instead of as a separate stream.  Used
+  // on level 0, whose b changes once per time step; the dense b stays the canonical
+  // copy and is scattered into the records on demand (sync_brec).
+  bool brec = false;
+  bool brec_ok = false;
 };
 
 template <typename T>
@@ -271,9 +277,11 @@ class Solver final : public SolverBase {
       // coefficient records, point-interleaved (mad_kernels.hpp, cidx); 3D levels keep
       // GHOST coefficient planes per side: neighbour planes on rank slabs (the fused
       // sweep recomputes colours on them), padding for masked border lanes otherwise
-      const int64_t cplane = L.g.sz * ncoef_;
+      L.brec = (dim == 3 && l == 0);
+      L.g.rs = ncoef_ + (L.brec ? 1 : 0);
+      const int64_t cplane = L.g.sz * L.g.rs;
       const int64_t cgp = (dim == 3) ? GHOST : 0;
-      const int64_t cmargin = margin * ncoef_;
+      const int64_t cmargin = margin * L.g.rs;
       const int64_t ctot = (L.g.nz + 2 * cgp) * cplane + 2 * cmargin;
       HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * ctot));
       HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
@@ -301,7 +309,7 @@ class Solver final : public SolverBase {
 
   void upload(int l, int which, const double* h) override {
     LevelData<T>& L = lv_[l];
-    if (which == MAD_B) L.b_halo_ok = false;
+    if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
     double* tmp = scratch64(L.g.N);
     HIP_CHECK(hipMemcpyAsync(tmp, h, sizeof(double) * L.g.N, hipMemcpyHostToDevice, c_->stream));
     hipLaunchKernelGGL((convert_k<double, T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream,
@@ -322,7 +330,7 @@ class Solver final : public SolverBase {
 
   void fill(int l, int which, double v) override {
     LevelData<T>& L = lv_[l];
-    if (which == MAD_B) L.b_halo_ok = false;
+    if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
     hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, arr(l, which),
                        L.g.N, (T)v);
     HIP_CHECK(hipGetLastError());
@@ -330,7 +338,7 @@ class Solver final : public SolverBase {
 
   void synth_level(int l, int which, uint64_t seed) override {
     LevelData<T>& L = lv_[l];
-    if (which == MAD_B) L.b_halo_ok = false;
+    if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
     const LevelGeom& G = c_->geom[l];
     hipLaunchKernelGGL((synth_image_k<T>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK), BLK, 0, c_->stream,
                        arr(l, which), L.g, G.n[0], G.n[1], seed);
@@ -437,7 +445,9 @@ class Solver final : public SolverBase {
       hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
                          zc, ntx, nty);
     };
-    if (KD == KFULL && fc.lead == 3)
+    if (L.brec)
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
+    else if (KD == KFULL && fc.lead == 3)
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>);
     else
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
@@ -466,18 +476,41 @@ class Solver final : public SolverBase {
         if (fc.tile == 2) { tx = 128; ty = 16; nt = 1024; }
         if (fc.tile == 3) { tx = 128; ty = 8; nt = 512; }
       }
-      const int lead = (kind == KFULL && fc.lead == 3) ? 3 : 2;
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d>", tn, kind, tx, ty,
-                    nt, sizeof(T) == 8 ? 2 : 4, lead);
+      const bool brec = lv_[l].brec;
+      const int lead = (!brec && kind == KFULL && fc.lead == 3) ? 3 : 2;
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d%s>", tn, kind, tx, ty,
+                    nt, sizeof(T) == 8 ? 2 : 4, lead, brec ? ", true" : "");
     }
     return buf;
+  }
+
+  // scatter the dense b into the records' b slot when it changed (brec levels); on a
+  // rank slab the ghost planes get the neighbours' b too (exchanged first)
+  void sync_brec(int l) {
+    LevelData<T>& L = lv_[l];
+    if (!L.brec || L.brec_ok) return;
+    int p0 = 0, p1 = L.g.nz;
+    if (c_->comm.active() && c_->geom[l].distributed) {
+      if (!L.b_halo_ok) {
+        halo(l, L.b, GHOST);
+        L.b_halo_ok = true;
+      }
+      if (L.g.zlo_ghost) p0 = -GHOST;
+      if (L.g.zhi_ghost) p1 = L.g.nz + GHOST;
+    }
+    dim3 gr = grid_for(L.g.nx, L.g.ny, p1 - p0, BLK);
+    hipLaunchKernelGGL((brec_scatter_k<T>), gr, BLK, 0, c_->stream, L.b, L.cf, L.g, ncoef_, p0);
+    HIP_CHECK(hipGetLastError());
+    L.brec_ok = true;
   }
 
   // one fused GS sweep x -> t, then swap (gs_fused_k)
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
-    if (!L.b_halo_ok) {
+    if (L.brec && c_->d.gs_kernel != 2) {
+      sync_brec(l);
+    } else if (!L.b_halo_ok) {
       halo(l, L.b, GHOST);
       L.b_halo_ok = true;
     }
@@ -571,10 +604,17 @@ class Solver final : public SolverBase {
       chunks = (L.g.nz + zc - 1) / zc;
       nparts = (int64_t)ntx * nty * chunks;
       REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
+      sync_brec(l);
       auto go = [&](auto K) {
-        hipLaunchKernelGGL((resid3_k<T, decltype(K)::value, TX, TY>), dim3((unsigned)nparts),
-                           dim3(TX * TY), 0, c_->stream, L.x, L.b, L.r, L.cf, L.g, L.rat, zc, ntx,
-                           want_norm ? part_ : nullptr);
+        constexpr int KD = decltype(K)::value;
+        if (L.brec)
+          hipLaunchKernelGGL((resid3_k<T, KD, TX, TY, true>), dim3((unsigned)nparts),
+                             dim3(TX * TY), 0, c_->stream, L.x, L.b, L.r, L.cf, L.g, L.rat, zc, ntx,
+                             want_norm ? part_ : nullptr);
+        else
+          hipLaunchKernelGGL((resid3_k<T, KD, TX, TY>), dim3((unsigned)nparts), dim3(TX * TY), 0,
+                             c_->stream, L.x, L.b, L.r, L.cf, L.g, L.rat, zc, ntx,
+                             want_norm ? part_ : nullptr);
       };
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
@@ -606,7 +646,7 @@ class Solver final : public SolverBase {
   void restrict_arr(int l, T* fine, T* coarse) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
-    C.b_halo_ok = false;
+    C.b_halo_ok = C.brec_ok = false;
     REQUIRE(!c_->geom[l].distributed || c_->geom[l + 1].distributed, MAD_ERR_UNSUPPORTED,
             "restriction onto a replicated level");
     halo(l, fine);
@@ -747,6 +787,7 @@ class Solver final : public SolverBase {
       vcycle_rec(0);
       return;
     }
+    sync_brec(0);  // eager: level 0's b changes between cycles (time steps), not inside
     if (!vgraph_) {
       struct Snap {
         T* x;
@@ -798,7 +839,7 @@ class Solver final : public SolverBase {
       }
     }
     HIP_CHECK(hipGraphLaunch(vgraph_, c_->stream));
-    for (size_t l = 1; l < lv_.size(); ++l) lv_[l].b_halo_ok = false;  // as the eager cycle
+    for (size_t l = 1; l < lv_.size(); ++l) lv_[l].b_halo_ok = lv_[l].brec_ok = false;  // as eager
   }
 
   void vcycle() override { vcycle_fast(); }
@@ -838,7 +879,7 @@ class Solver final : public SolverBase {
       src = stage;
     }
     convert_in(src, in_dtype, L0.b, N);
-    L0.b_halo_ok = false;
+    L0.b_halo_ok = L0.brec_ok = false;
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
@@ -892,7 +933,7 @@ class Solver final : public SolverBase {
       c_->step_relres.push_back(relres);
       HIP_CHECK(hipMemcpyAsync(L0.b, L0.x, sizeof(T) * N, hipMemcpyDeviceToDevice,
                                c_->stream));  // MAD.hxx:248-261
-      L0.b_halo_ok = false;
+      L0.b_halo_ok = L0.brec_ok = false;
     }
     HIP_CHECK(hipEventRecord(e1, c_->stream));
     // cast solution -> output type (MAD.hxx:266-289)
@@ -1134,21 +1175,21 @@ class Solver final : public SolverBase {
       const bool slab = (L.g.N != Ng);
       T* dst = L.cf;
       if (slab) {
-        HIP_CHECK(hipMalloc(&full_cf, sizeof(T) * Ng * ncoef_));
+        HIP_CHECK(hipMalloc(&full_cf, sizeof(T) * Ng * L.g.rs));
         dst = full_cf;
       }
       dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
       dispatch(dim, c_->kind, [&](auto D, auto K) {
         hipLaunchKernelGGL((build_coef_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
                            (int)G.n[0], (int)G.n[1], (int)G.n[2], G.h[0], G.h[1], G.h[2],
-                           c_->d.time_step, dst);
+                           c_->d.time_step, dst, L.g.rs);
       });
       HIP_CHECK(hipGetLastError());
       if (slab) {
         // owned planes plus up to GHOST neighbour planes on each side (whole plane blocks)
         const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
         const int64_t p1 = std::min<int64_t>(G.z1 + GHOST, G.n[2]);
-        const int64_t cplane = L.g.sz * ncoef_;
+        const int64_t cplane = L.g.sz * L.g.rs;
         HIP_CHECK(hipMemcpyAsync(L.cf + (p0 - G.z0) * cplane, full_cf + p0 * cplane,
                                  sizeof(T) * (p1 - p0) * cplane, hipMemcpyDeviceToDevice,
                                  c_->stream));
@@ -1174,7 +1215,7 @@ class Solver final : public SolverBase {
     dispatch(dim, c_->kind, [&](auto D, auto K) {
       hipLaunchKernelGGL((build_coef_k<double, D.value, K.value>), gr, BLK, 0, c_->stream,
                          tensor_l, (int)G.n[0], (int)G.n[1], (int)G.n[2], G.h[0], G.h[1], G.h[2],
-                         c_->d.time_step, cf64);
+                         c_->d.time_step, cf64, nc);
     });
     HIP_CHECK(hipGetLastError());
     coarse_coef64_.resize((size_t)G.N * nc);
@@ -1277,7 +1318,7 @@ class Solver final : public SolverBase {
   void restrict_full(int l, const T* fine_full, T* coarse) {
     const LevelGeom& Gf = c_->geom[l];
     LevelData<T>& C = lv_[l + 1];
-    C.b_halo_ok = false;
+    C.b_halo_ok = C.brec_ok = false;
     Geo gf{};
     gf.nx = (int)Gf.n[0]; gf.ny = (int)Gf.n[1]; gf.nz = (int)Gf.n[2];
     gf.sy = Gf.n[0]; gf.sz = Gf.n[0] * Gf.n[1]; gf.N = Gf.N;
