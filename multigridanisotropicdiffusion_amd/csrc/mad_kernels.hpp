@@ -580,7 +580,8 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
 template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
-                                                        Geo g, Rat<T> rat, int zc, int ntx, int nty) {
+                                                        Geo g, Rat<T> rat, int zc, int ntx, int nty,
+                                                        int zbase, int zstride) {
   constexpr int NC = (KIND == KFULL) ? 4 : 2;
   using FG = FusedGeom<NC, TX, TY>;
   constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
@@ -617,7 +618,9 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;
   const int ulo = g.zlo_ghost ? -(GHOST - 1) : 0;
   const int uhi = g.zhi_ghost ? g.nz + GHOST - 1 : g.nz;
-  const int z0 = chunk * zc;
+  // chunk q of this launch covers owned planes [zbase + q*zstride, +zc): one launch
+  // may cover a slab's two boundary chunks only, or its interior (rank-slab overlap)
+  const int z0 = zbase + chunk * zstride;
   const int z1 = min(z0 + zc, g.nz);
   // first step with its plane parity normalised to even (global z), last step
   const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + g.zoff) & 1);
@@ -1354,7 +1357,8 @@ __global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fin
 template <typename T, int ADD, int TX, int TY>
 __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coarse, Geo gc,
                                                      T* __restrict__ fine, Geo gf, int cx, int cy,
-                                                     int cz, int ncz, int kc, int ntx) {
+                                                     int cz, int ncz, int kc, int ntx, int kbase,
+                                                     int kend) {
 #pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   constexpr int NT = TX * TY;
   constexpr int CXW = TX / 2 + 2, CYW = TY / 2 + 2, CP = CXW * CYW;
@@ -1375,7 +1379,9 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
   const int ci = tid < CP ? tid : CP - 1;  // one ring element per thread (CP <= NT)
   const int c_off = min(max(cy0 + ci / CXW, 0), gc.ny - 1) * (int)gc.sy +
                     min(max(cx0 + ci % CXW, 0), gc.nx - 1);
-  const int k0 = chunk * kc, k1 = min(k0 + kc, gf.nz);
+  // fine planes [kbase, kend), local; on a rank slab the range may include the ghost
+  // planes (their coarse taps then reach up to 3 coarse ghost planes)
+  const int k0 = kbase + chunk * kc, k1 = min(k0 + kc, kend);
   const int64_t pxy = (int64_t)j * gf.sy + i;
   int last = INT_MIN;  // largest coarse plane (global) in the ring
   T xn = (ADD && ok && k0 < k1) ? fine[pxy + gf.sz * (int64_t)k0] : T(0);
@@ -1383,7 +1389,7 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
     int iz[2], jz[2];
     T wz[2], vz2[2];
     itaps2<T>(k + gf.zoff, ncz, cz, iz, wz);
-    itaps2<T>(min(k + 1, gf.nz - 1) + gf.zoff, ncz, cz, jz, vz2);
+    itaps2<T>(min(k + 1, kend - 1) + gf.zoff, ncz, cz, jz, vz2);
     // coarse planes min(iz)..max(jz) not yet in the ring (even fine planes have taps
     // {K, K-1}: not ordered, so ranges)
     const int need_hi = max(max(iz[0], iz[1]), max(jz[0], jz[1]));

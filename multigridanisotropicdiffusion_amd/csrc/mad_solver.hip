@@ -158,6 +158,7 @@ struct mad_ctx {
   std::string err;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t comm_stream = nullptr;  // overlapped halo exchanges (rank slabs)
   int dim = 3;
   int nlev = 0;
   std::vector<LevelGeom> geom;
@@ -202,6 +203,7 @@ mad_ctx::~mad_ctx() {
   if (tensor64) (void)hipFree(tensor64);
   comm.destroy();
   if (stream) (void)hipStreamDestroy(stream);
+  if (comm_stream) (void)hipStreamDestroy(comm_stream);
 }
 
 namespace {
@@ -226,7 +228,14 @@ struct LevelData {
   // copy and is scattered into the records on demand (sync_brec).
   bool brec = false;
   bool brec_ok = false;
+  // rank slabs: x's GHOST ghost planes hold the neighbours' current x (x_halo_ok),
+  // possibly still being written by the overlapped exchange (x_halo_pending, ev_halo)
+  bool x_halo_ok = false;
+  bool x_halo_pending = false;
+  hipEvent_t ev_bnd = nullptr;   // boundary chunks of the fused sweep done
+  hipEvent_t ev_halo = nullptr;  // their exchange done (communication stream)
 };
+constexpr int kBoundaryPlanes = 8;  // z-depth of a rank slab's boundary chunks (>= GHOST)
 
 template <typename T>
 class Solver final : public SolverBase {
@@ -289,6 +298,11 @@ class Solver final : public SolverBase {
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
+    for (int l = 0; l < nl; ++l)
+      if (c->geom[l].distributed) {
+        HIP_CHECK(hipEventCreateWithFlags(&lv_[l].ev_bnd, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&lv_[l].ev_halo, hipEventDisableTiming));
+      }
     part_need = std::max<int64_t>(part_need, 4096);
     HIP_CHECK(hipMalloc(&part_, sizeof(double) * part_need));
     part_cap_ = part_need;
@@ -310,6 +324,7 @@ class Solver final : public SolverBase {
   void upload(int l, int which, const double* h) override {
     LevelData<T>& L = lv_[l];
     if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
+    if (which == MAD_X) x_changed(l);
     double* tmp = scratch64(L.g.N);
     HIP_CHECK(hipMemcpyAsync(tmp, h, sizeof(double) * L.g.N, hipMemcpyHostToDevice, c_->stream));
     hipLaunchKernelGGL((convert_k<double, T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream,
@@ -331,6 +346,7 @@ class Solver final : public SolverBase {
   void fill(int l, int which, double v) override {
     LevelData<T>& L = lv_[l];
     if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
+    if (which == MAD_X) x_changed(l);
     hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, arr(l, which),
                        L.g.N, (T)v);
     HIP_CHECK(hipGetLastError());
@@ -339,6 +355,7 @@ class Solver final : public SolverBase {
   void synth_level(int l, int which, uint64_t seed) override {
     LevelData<T>& L = lv_[l];
     if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
+    if (which == MAD_X) x_changed(l);
     const LevelGeom& G = c_->geom[l];
     hipLaunchKernelGGL((synth_image_k<T>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK), BLK, 0, c_->stream,
                        arr(l, which), L.g, G.n[0], G.n[1], seed);
@@ -346,12 +363,30 @@ class Solver final : public SolverBase {
   }
 
   // halo exchange of `depth` boundary planes of one array (multi-GPU; no-op on one rank)
+  // The main stream waits for every overlapped exchange still in flight.  Called
+  // before any communication is issued on the main stream: RCCL operations on one
+  // communicator must run in the same order on every rank, so two of them may never
+  // be in flight on different streams at once.
+  void wait_all_pending() {
+    for (auto& L : lv_)
+      if (L.x_halo_pending) {
+        HIP_CHECK(hipStreamWaitEvent(c_->stream, L.ev_halo, 0));
+        L.x_halo_pending = false;
+      }
+  }
+
   void halo(int l, T* a, int depth = 1) {
     if (!c_->comm.active() || !c_->geom[l].distributed) return;
     LevelData<T>& L = lv_[l];
+    wait_all_pending();
+    if (a == L.x && L.x_halo_ok && depth <= GHOST) return;  // ghost planes are current
     c_->comm.exchange_planes(a, L.g.sz, L.g.nz, depth, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
                              std::is_same<T, double>::value, c_->stream);
+    if (a == L.x && depth == GHOST) L.x_halo_ok = true;
   }
+
+  // level l's x changed without its ghost planes (they must be exchanged again)
+  void x_changed(int l) { lv_[l].x_halo_ok = false; }
 
   // target grid size of the z-marching transfer kernels (MAD_XFER_BLOCKS, tuning)
   static int xfer_blocks() {
@@ -411,20 +446,40 @@ class Solver final : public SolverBase {
     return c;
   }
 
+  // z-range of one fused launch: chunks q = 0..nchunks-1 cover owned planes
+  // [zbase + q*zstride, + zc)
+  struct ZRange {
+    int zbase, zc, zstride, nchunks;
+  };
+  // the whole slab in chunks sized for ~fc.blocks workgroups (at least 32 planes)
+  static ZRange whole_range(int nz, int tiles, const FusedCfg& fc) {
+    int chunks = (fc.blocks + tiles - 1) / tiles;
+    chunks = std::max(1, std::min(chunks, std::max(1, nz / 32)));
+    const int zc = (nz + chunks - 1) / chunks;
+    return ZRange{0, zc, zc, (nz + zc - 1) / zc};
+  }
+
   template <int KD, int TX, int TY, int NT>
-  void launch_fused(LevelData<T>& L, const FusedCfg& fc) {
+  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
-    int chunks = (fc.blocks + tiles - 1) / tiles;
-    chunks = std::max(1, std::min(chunks, std::max(1, L.g.nz / 32)));
-    const int zc = (L.g.nz + chunks - 1) / chunks;
-    chunks = (L.g.nz + zc - 1) / zc;
-    const unsigned nb = (unsigned)(tiles * chunks);
+    const int nz = L.g.nz;
+    ZRange zr = whole_range(nz, tiles, fc);
+    if (part == 1) {  // the two boundary chunks of a rank slab (they produce the halo planes)
+      zr = ZRange{0, kBoundaryPlanes, nz - kBoundaryPlanes, 2};
+    } else if (part == 2) {  // the interior between them
+      const int ni = nz - 2 * kBoundaryPlanes;
+      int chunks = std::max(1, std::min((fc.blocks + tiles - 1) / tiles, std::max(1, ni / 16)));
+      const int zc = (ni + chunks - 1) / chunks;
+      zr = ZRange{kBoundaryPlanes, zc, zc, (ni + zc - 1) / zc};
+    }
+    const unsigned nb = (unsigned)(tiles * zr.nchunks);
     if (c_->d.gs_kernel == 2) {
+      REQUIRE(part == 0, MAD_ERR_UNSUPPORTED, "fused v2 sweeps the whole slab");
       hipLaunchKernelGGL((gs_fused_k<T, KD, 64, 16, (KD == KFULL ? 512 : 1024), 4>),
-                         dim3((unsigned)(((L.g.nx + 63) / 64) * ((L.g.ny + 15) / 16) * chunks)),
+                         dim3((unsigned)(((L.g.nx + 63) / 64) * ((L.g.ny + 15) / 16) * zr.nchunks)),
                          dim3(KD == KFULL ? 512 : 1024), 0, c_->stream, L.x, L.t, L.b, L.cf, L.g,
-                         L.rat, zc, (L.g.nx + 63) / 64, (L.g.ny + 15) / 16);
+                         L.rat, zr.zc, (L.g.nx + 63) / 64, (L.g.ny + 15) / 16);
       return;
     }
     constexpr int NC = (KD == KFULL) ? 4 : 2;
@@ -443,7 +498,7 @@ class Solver final : public SolverBase {
         attr = true;
       }
       hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zc, ntx, nty);
+                         zr.zc, ntx, nty, zr.zbase, zr.zstride);
     };
     if (L.brec)
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
@@ -451,6 +506,25 @@ class Solver final : public SolverBase {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>);
     else
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+  }
+
+  void launch_fused_part(LevelData<T>& L, int part) {
+    const FusedCfg& fc = fused_cfg();
+    if (c_->kind == KFULL) {
+      if (fc.tile == 1)
+        launch_fused<KFULL, 64, 32, 1024>(L, fc, part);
+      else if (fc.tile == 2)
+        launch_fused<KFULL, 128, 16, 1024>(L, fc, part);
+      else if (fc.tile == 3)
+        launch_fused<KFULL, 128, 8, 512>(L, fc, part);
+      else
+        launch_fused<KFULL, 64, 16, 512>(L, fc, part);
+    } else if (c_->kind == KDIAG) {
+      launch_fused<KDIAG, 64, 16, 1024>(L, fc, part);
+    } else {
+      launch_fused<KISO, 64, 16, 1024>(L, fc, part);
+    }
+    HIP_CHECK(hipGetLastError());
   }
 
   // rocprof-style name of the kernel one level-l sweep launches (bench / profiles)
@@ -505,6 +579,12 @@ class Solver final : public SolverBase {
   }
 
   // one fused GS sweep x -> t, then swap (gs_fused_k)
+  // One fused GS sweep x -> t, then swap.  On a rank slab the halo exchange of the NEW
+  // x is overlapped with the sweep: the two boundary chunks (which produce the planes
+  // the neighbours need) run first, the exchange of their output then runs on the
+  // communication stream while the interior chunks sweep, and the next consumer of
+  // x's ghost planes waits for it (halo()).  Slabs thinner than 3 boundary chunks
+  // sweep in one launch and exchange afterwards.
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
@@ -515,25 +595,29 @@ class Solver final : public SolverBase {
       L.b_halo_ok = true;
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
-    const FusedCfg& fc = fused_cfg();
-    if (c_->kind == KFULL) {
-      if (fc.tile == 1)
-        launch_fused<KFULL, 64, 32, 1024>(L, fc);
-      else if (fc.tile == 2)
-        launch_fused<KFULL, 128, 16, 1024>(L, fc);
-      else if (fc.tile == 3)
-        launch_fused<KFULL, 128, 8, 512>(L, fc);
-      else
-        launch_fused<KFULL, 64, 16, 512>(L, fc);
-    } else if (c_->kind == KDIAG) {
-      launch_fused<KDIAG, 64, 16, 1024>(L, fc);
+    const bool dist = c_->comm.active() && c_->geom[l].distributed;
+    const bool overlap = dist && c_->d.gs_kernel != 2 && L.g.nz >= 3 * kBoundaryPlanes;
+    if (!overlap) {
+      launch_fused_part(L, 0);
     } else {
-      launch_fused<KISO, 64, 16, 1024>(L, fc);
+      launch_fused_part(L, 1);
+      wait_all_pending();  // (none expected: halo() above already waited)
+      HIP_CHECK(hipEventRecord(L.ev_bnd, c_->stream));
+      HIP_CHECK(hipStreamWaitEvent(c_->comm_stream, L.ev_bnd, 0));
+      c_->comm.exchange_planes(L.t, L.g.sz, L.g.nz, GHOST, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
+                               std::is_same<T, double>::value, c_->comm_stream);
+      HIP_CHECK(hipEventRecord(L.ev_halo, c_->comm_stream));
+      launch_fused_part(L, 2);
     }
     if (e1) HIP_CHECK(hipEventRecord(e1, c_->stream));
-    HIP_CHECK(hipGetLastError());
     std::swap(L.x, L.t);
     std::swap(L.alloc[0], L.alloc[3]);
+    if (overlap) {
+      L.x_halo_ok = true;
+      L.x_halo_pending = true;
+    } else {
+      L.x_halo_ok = false;
+    }
     return 0.f;
   }
 
@@ -552,6 +636,7 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipGetLastError());
         std::swap(L.x, L.t);
         std::swap(L.alloc[0], L.alloc[3]);
+        x_changed(l);
       } else if (sm == MAD_GAUSS_SEIDEL_LEX) {
         REQUIRE(!c_->comm.active(), MAD_ERR_UNSUPPORTED,
                 "lexicographic GS is a single-GPU parity mode");
@@ -576,6 +661,7 @@ class Solver final : public SolverBase {
             hipLaunchKernelGGL((gs_color_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, L.x,
                                L.b, L.cf, L.g, L.rat, col, nc);
           });
+          x_changed(l);
         }
         HIP_CHECK(hipGetLastError());
       }
@@ -585,7 +671,10 @@ class Solver final : public SolverBase {
   double finish_norm2(int64_t nparts, bool global) {
     hipLaunchKernelGGL(reduce_final_k, dim3(1), dim3(256), 0, c_->stream, part_, nparts, scal_);
     HIP_CHECK(hipGetLastError());
-    if (global && c_->comm.active()) c_->comm.allreduce_sum_f64(scal_, 1, c_->stream);
+    if (global && c_->comm.active()) {
+      wait_all_pending();
+      c_->comm.allreduce_sum_f64(scal_, 1, c_->stream);
+    }
     HIP_CHECK(hipMemcpyAsync(hscal_, scal_, sizeof(double), hipMemcpyDeviceToHost, c_->stream));
     HIP_CHECK(hipStreamSynchronize(c_->stream));
     return hscal_[0];
@@ -676,10 +765,13 @@ class Solver final : public SolverBase {
   void interpolate(int l, bool add) override {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
-    halo(l + 1, C.x);
+    const bool ghosts = interp_ghosts(l, add);
+    halo(l + 1, C.x, ghosts ? 3 : 1);  // fine ghost planes reach 3 coarse planes out
     dim3 gr = grid_for(F.g.nx, F.g.ny, F.g.nz, BLK);
     if (c_->dim == 3) {
-      launch_interp3(l, add);
+      launch_interp3(l, add, ghosts);
+      if (ghosts) F.x_halo_ok = true;
+      else x_changed(l);
     } else {
       if (add)
         hipLaunchKernelGGL((interp_k<T, 2, 1>), gr, BLK, 0, c_->stream, C.x, C.g, F.x, F.g,
@@ -898,6 +990,7 @@ class Solver final : public SolverBase {
       } else {
         HIP_CHECK(hipMemcpyAsync(L0.x, L0.b, sizeof(T) * N, hipMemcpyDeviceToDevice,
                                  c_->stream));  // MAD.hxx:177-201
+        x_changed(0);
       }
       const double rhsNorm = norm(0, MAD_B);  // MAD.hxx:204
       unsigned it = 0;
@@ -993,6 +1086,7 @@ class Solver final : public SolverBase {
         ++q;
         std::swap(L.x, L.t);
         std::swap(L.alloc[0], L.alloc[3]);
+        x_changed(l);
       } else if (fused) {
         fused_sweep(l, ev[2 * q], ev[2 * q + 1]);
         ++q;
@@ -1007,10 +1101,15 @@ class Solver final : public SolverBase {
           });
           HIP_CHECK(hipEventRecord(ev[2 * q + 1], c_->stream));
           ++q;
+          x_changed(l);
         }
       }
     }
     HIP_CHECK(hipGetLastError());
+    if (L.x_halo_pending) {  // the last overlapped exchange belongs to the timed work
+      HIP_CHECK(hipStreamWaitEvent(c_->stream, L.ev_halo, 0));
+      L.x_halo_pending = false;
+    }
     HIP_CHECK(hipEventRecord(z, c_->stream));
     HIP_CHECK(hipEventSynchronize(z));
     float ms = 0.f;
@@ -1063,10 +1162,13 @@ class Solver final : public SolverBase {
   int64_t gathered_cap_ = 0;
 
   void release() {
+    if (c_ && c_->comm_stream) (void)hipStreamSynchronize(c_->comm_stream);
     if (vgraph_) (void)hipGraphExecDestroy(vgraph_);
     vgraph_ = nullptr;
     vgraph_failed_ = false;
     for (auto& L : lv_) {
+      if (L.ev_bnd) (void)hipEventDestroy(L.ev_bnd);
+      if (L.ev_halo) (void)hipEventDestroy(L.ev_halo);
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
@@ -1312,6 +1414,7 @@ class Solver final : public SolverBase {
   void gather_level(int l, const T* a) {
     const LevelGeom& G = c_->geom[l];
     ensure_gather(G.N);
+    wait_all_pending();
     c_->comm.allgather_slabs(a, gathered_, G.n[0] * G.n[1], G.n[2], sizeof(T), c_->stream);
   }
 
@@ -1330,28 +1433,46 @@ class Solver final : public SolverBase {
 
   // fine slab (distributed) from the replicated coarse level
   void interp_from_replicated(int l, bool add) {
-    launch_interp3(l, add);
+    const bool ghosts = interp_ghosts(l, add);
+    launch_interp3(l, add, ghosts);
     HIP_CHECK(hipGetLastError());
+    if (ghosts) lv_[l].x_halo_ok = true;
+    else x_changed(l);
   }
 
   // x[l] (+)= P x[l+1], 3D, z-marching (interp3_k): 64x16 fine columns, ~1024 blocks.
   // The coarse level may be a slab (ghost planes exchanged) or replicated (zoff 0).
-  void launch_interp3(int l, bool add) {
+  void launch_interp3(int l, bool add, bool ghosts = false) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
     constexpr int TX = 64, TY = 16;
+    const int kbase = (ghosts && F.g.zlo_ghost) ? -GHOST : 0;
+    const int kend = (ghosts && F.g.zhi_ghost) ? F.g.nz + GHOST : F.g.nz;
+    const int nk = kend - kbase;
     const int ntx = (F.g.nx + TX - 1) / TX, nty = (F.g.ny + TY - 1) / TY;
-    int chunks = std::max(1, std::min((xfer_blocks() + ntx * nty - 1) / (ntx * nty), F.g.nz / 4));
-    const int kc = (F.g.nz + chunks - 1) / chunks;
-    chunks = (F.g.nz + kc - 1) / kc;
+    int chunks = std::max(1, std::min((xfer_blocks() + ntx * nty - 1) / (ntx * nty), nk / 4));
+    const int kc = (nk + chunks - 1) / chunks;
+    chunks = (nk + kc - 1) / kc;
     const unsigned nb = (unsigned)(ntx * nty * chunks);
     const int ncz = (int)c_->geom[l + 1].n[2];
     if (add)
       hipLaunchKernelGGL((interp3_k<T, 1, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
-                         C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx);
+                         C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx, kbase, kend);
     else
       hipLaunchKernelGGL((interp3_k<T, 0, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
-                         C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx);
+                         C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx, kbase, kend);
+  }
+
+  // On a rank slab whose ghost planes are current, interpolation updates them too
+  // (the neighbours' x + P e, computed from the exchanged x and coarse ghost planes:
+  // the same values the neighbours compute), so the post-smoothing sweep needs no
+  // exchange first.  Returns whether it does (the caller passes it to launch_interp3).
+  bool interp_ghosts(int l, bool add) {
+    LevelData<T>& F = lv_[l];
+    if (!c_->comm.active() || !c_->geom[l].distributed || c_->dim != 3) return false;
+    if (add && !F.x_halo_ok) return false;
+    wait_all_pending();  // the ghost planes may still be arriving
+    return true;
   }
 };
 
@@ -1517,6 +1638,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
     c->device = dev;
     use_device(c.get());
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     compute_geometry(c.get());
   });
   if (rc != MAD_OK) return rc;
@@ -1780,6 +1902,7 @@ int mad_synchronize(mad_ctx* c) {
   return guarded(c, [&] {
     use_device(c);
     HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->comm_stream));
   });
 }
 
