@@ -1061,7 +1061,7 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
     const T rv = resid_value(BREC ? raw[NCF] : bv, D, P0[0], S);
     load_pt(m + 1);
     if (ok) {
-      buf_store<T>(rv, buf_rsrc(r + (int64_t)m * sz + pbase), pt_off);
+      if (r) buf_store<T>(rv, buf_rsrc(r + (int64_t)m * sz + pbase), pt_off);  // null: norm only
       sq += (double)rv * (double)rv;
     }
   }

@@ -680,7 +680,11 @@ class Solver final : public SolverBase {
     return hscal_[0];
   }
 
-  double residual(int l, bool want_norm) override {
+  double residual(int l, bool want_norm) override { return residual_impl(l, want_norm, true); }
+
+  // write_r false: only ||r|| is wanted (the per-cycle convergence test), r is not
+  // stored (z-marching path; the per-point fallback always stores it)
+  double residual_impl(int l, bool want_norm, bool write_r) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x);
     int64_t nparts = 0;
@@ -696,13 +700,14 @@ class Solver final : public SolverBase {
       sync_brec(l);
       auto go = [&](auto K) {
         constexpr int KD = decltype(K)::value;
+        T* rout = write_r ? L.r : nullptr;
         if (L.brec)
           hipLaunchKernelGGL((resid3_k<T, KD, TX, TY, true>), dim3((unsigned)nparts),
-                             dim3(TX * TY), 0, c_->stream, L.x, L.b, L.r, L.cf, L.g, L.rat, zc, ntx,
+                             dim3(TX * TY), 0, c_->stream, L.x, L.b, rout, L.cf, L.g, L.rat, zc, ntx,
                              want_norm ? part_ : nullptr);
         else
           hipLaunchKernelGGL((resid3_k<T, KD, TX, TY>), dim3((unsigned)nparts), dim3(TX * TY), 0,
-                             c_->stream, L.x, L.b, L.r, L.cf, L.g, L.rat, zc, ntx,
+                             c_->stream, L.x, L.b, rout, L.cf, L.g, L.rat, zc, ntx,
                              want_norm ? part_ : nullptr);
       };
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
@@ -1005,7 +1010,7 @@ class Solver final : public SolverBase {
           if (d.verbose && c_->comm.rank() == 0) std::printf("\n|--- VCycle n. %u ---|\n", it + 1);
           vcycle_fast();
         }
-        relres = residual(0, true) / rhsNorm;
+        relres = residual_impl(0, true, false) / rhsNorm;  // MAD.hxx:221-229 (norm only)
         if (d.verbose && d.cycle == MAD_SMOOTHER && c_->comm.rank() == 0)
           std::printf("Smoother iteration n. %u: relative residual = %g\n", it + 1, relres);
         ++it;
