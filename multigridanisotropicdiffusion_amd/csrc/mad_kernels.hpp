@@ -1189,85 +1189,22 @@ __global__ void __launch_bounds__(256) interp_k(const T* __restrict__ coarse, Ge
   else fine[p] = v;
 }
 
-// 3D slab versions: z taps are computed from GLOBAL plane indices (zoff) and the
-// global coarse depth ncz; local plane -1 / nz are the ghost planes (filled by the
-// halo exchange before the launch).  On one GPU zoff = 0 and the slab is the grid.
+// 3D transfers on a z-slab: z taps are computed from GLOBAL plane indices (zoff) and
+// the global coarse depth ncz; local plane -1 / nz are the ghost planes (filled by
+// the halo exchange before the launch).  On one GPU zoff = 0 and the slab is the grid.
 // Taps are held in registers with a fixed count per axis (4 for restriction, 2 for
-// interpolation; unused taps weigh 0): the tap loops unroll completely.  Same
-// inter-grid stencils of the reference (itkInterGridOperators.h:101-127; restriction
-// taps IGO.h:115-127, interpolation scatter stencils IGO.h:101-113 as gathers):
+// interpolation; unused taps weigh 0) and summed x, then y, then z with explicit fma,
+// the same order as the 2D / generic kernels above.  Same inter-grid stencils of the
+// reference (itkInterGridOperators.h:101-127; restriction taps IGO.h:115-127,
+// interpolation scatter stencils IGO.h:101-113 as gathers):
 //   cell-centred restriction = 1/8,3/8,3/8,1/8 on 2I-1..2I+2 with the fine index
 //   clamped into the grid (which reproduces the one-sided border rows exactly);
 //   vertex-centred = 1/4,1/2,1/4 about 2I, injection at both ends.
 //   cell-centred interpolation = 3/4 c(I) + 1/4 c(I -+ 1), coarse index clamped;
 //   vertex-centred = c(f/2) for even f, (c(f/2) + c(f/2+1)) / 2 for odd f.
-template <typename T, typename A>
-__global__ void __launch_bounds__(256) restrict_slab_k(const T* __restrict__ fine, Geo gf,
-                                                       T* __restrict__ coarse, Geo gc, int cx,
-                                                       int cy, int cz, int fz_shift, int ncz) {
-#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
-  const int K = blockIdx.z;
-  const int J = blockIdx.y * blockDim.y + threadIdx.y;
-  const int I = blockIdx.x * blockDim.x + threadIdx.x;
-  if (I >= gc.nx || J >= gc.ny) return;
-  int ix[4], iy[4], iz[4];
-  A wx[4], wy[4], wz[4];
-  rtaps4<A>(I, gc.nx, cx, ix, wx);
-  rtaps4<A>(J, gc.ny, cy, iy, wy);
-  rtaps4<A>(K + gc.zoff, ncz, cz, iz, wz);
-  A v = A(0);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const T* pl = fine + gf.sz * (int64_t)(iz[c] - fz_shift);
-    A vz = A(0);
-#pragma unroll
-    for (int bq = 0; bq < 4; ++bq) {
-      const T* row = pl + gf.sy * iy[bq];
-      A vy = A(0);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) vy = fma(wx[a], (A)row[ix[a]], vy);
-      vz = fma(wy[bq], vy, vz);
-    }
-    v = fma(wz[c], vz, v);
-  }
-  coarse[I + gc.sy * J + gc.sz * K] = (T)v;
-}
-
-template <typename T, int ADD>
-__global__ void __launch_bounds__(256) interp_slab_k(const T* __restrict__ coarse, Geo gc,
-                                                     T* __restrict__ fine, Geo gf, int cx, int cy,
-                                                     int cz, int ncz) {
-#pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
-  const int k = blockIdx.z;
-  const int j = blockIdx.y * blockDim.y + threadIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= gf.nx || j >= gf.ny) return;
-  int ix[2], iy[2], iz[2];
-  T wx[2], wy[2], wz[2];
-  itaps2<T>(i, gc.nx, cx, ix, wx);
-  itaps2<T>(j, gc.ny, cy, iy, wy);
-  itaps2<T>(k + gf.zoff, ncz, cz, iz, wz);
-  T v = T(0);
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const T* pl = coarse + gc.sz * (int64_t)(iz[c] - gc.zoff);
-    T vz = T(0);
-#pragma unroll
-    for (int bq = 0; bq < 2; ++bq) {
-      const T* row = pl + gc.sy * iy[bq];
-      vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
-    }
-    v = fma(wz[c], vz, v);
-  }
-  const int64_t p = i + gf.sy * j + gf.sz * k;
-  if (ADD) fine[p] += v;
-  else fine[p] = v;
-}
-
-// z-marching 3D transfers (same taps and summation order as restrict_slab_k /
-// interp_slab_k, so results are bit-identical): each workgroup owns a tile column,
-// stages one plane at a time in LDS (coalesced loads, each fine / coarse value read
-// once from HBM), and carries the z dimension in registers.
+// Both kernels march z: each workgroup owns a tile column, stages one plane at a
+// time in LDS (coalesced loads, each fine / coarse value read once from HBM), and
+// carries the z dimension in registers.
 //
 // restrict3_k: coarse tile CX x CY (one thread per coarse point), coarse planes
 // [K0, K1).  Marches the fine planes the chunk needs in order: each fine plane is

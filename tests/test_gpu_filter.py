@@ -171,3 +171,43 @@ def test_vcycle_convergence_factor_at_scale(M):
         assert factors and max(factors) < 0.2, rel
     # cycle 1 is well above the fp32 floor: both precisions follow the same history
     assert abs(res[M.FP32][1] - res[M.FP64][1]) < 0.05 * res[M.FP64][1]
+
+
+@pytest.mark.parametrize("precision", ["FP32", "FP64"])
+def test_baseline_config_c2_128_isotropic_wj(M, oracle_mod, precision):
+    """BASELINE.json configs[1]: 128^3 synthetic volume, isotropic (scalar) coefficients,
+    V-cycle with the weighted-Jacobi smoother; whole filter against the oracle at the
+    reference tolerance 1e-10.  (The level count follows the reference's depth rule,
+    itkMultigridAnisotropicDiffusionImageFilter.hxx GenerateData: 5 levels at 128^3.)"""
+    shape = (128, 128, 128)
+    T = synth.isotropic(shape)
+    x = synth.image(shape, seed=5)
+    o = oracle_mod.Oracle(shape, (1.0, 1.0, 1.0), T, 0.1)
+    ref, cyc, _ = o.run(x, tolerance=1e-10, smoother=oracle_mod.WJ)
+    s = M.Solver(shape, time_step=0.1, tolerance=1e-10, smoother=M.WEIGHTED_JACOBI,
+                 precision=getattr(M, precision))
+    s.set_tensor(T)
+    out, st = s.run(x, out_dtype=np.float64)
+    assert st["tensor_kind"] == 1 and s.num_levels == o.num_levels
+    assert relinf(out, ref) < (1e-5 if precision == "FP32" else 1e-9)
+    if precision == "FP64":
+        assert st["step_cycles"] == cyc and st["last_relres"] <= 1e-10
+
+
+def test_baseline_config_c3_256_full_tensor_gs(M, oracle_mod):
+    """BASELINE.json configs[2]: 256^3 synthetic volume, full 3x3 anisotropic tensor
+    (VED form), Gauss-Seidel smoother.  The GPU runs the multicolour GS in fp32, the
+    oracle the reference's lexicographic GS in fp64; both solve to 1e-10 (fp32 to its
+    rounding floor), so the solutions agree within the north-star 1e-5 relative."""
+    shape = (256, 256, 256)
+    T = synth.ved_form(shape)
+    x = synth.image(shape, seed=5).astype(np.float32)  # fp32 volume, same input to both
+    o = oracle_mod.Oracle(shape, (1.0, 1.0, 1.0), T, 0.1)
+    ref, _, _ = o.run(x.astype(np.float64), tolerance=1e-10)
+    del o
+    s = M.Solver(shape, time_step=0.1, tolerance=1e-10, precision=M.FP32)
+    s.set_tensor(T)
+    del T
+    out, st = s.run(x, out_dtype=np.float64)
+    assert st["tensor_kind"] == 3 and st["colors"] == 4
+    assert relinf(out, ref) < 1e-5
