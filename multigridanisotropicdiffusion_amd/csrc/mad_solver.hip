@@ -598,7 +598,15 @@ class Solver final : public SolverBase {
     const bool dist = c_->comm.active() && c_->geom[l].distributed;
     const bool overlap = dist && c_->d.gs_kernel != 2 && L.g.nz >= 3 * kBoundaryPlanes;
     if (!overlap) {
-      launch_fused_part(L, 0);
+      // MAD_SPLIT_PROXY=1 (measurement only): launch a single-GPU slab as a rank slab's
+      // boundary + interior parts, without the exchange (tools/bench_slab.py)
+      static const bool proxy = std::getenv("MAD_SPLIT_PROXY") != nullptr;
+      if (proxy && c_->d.gs_kernel != 2 && L.g.nz >= 3 * kBoundaryPlanes) {
+        launch_fused_part(L, 1);
+        launch_fused_part(L, 2);
+      } else {
+        launch_fused_part(L, 0);
+      }
     } else {
       launch_fused_part(L, 1);
       wait_all_pending();  // (none expected: halo() above already waited)
