@@ -1,0 +1,100 @@
+/*
+ * mad_ved.h -- C ABI of the VED (vessel enhancing diffusion) pipeline on the GPU:
+ * the caller of the multigrid hot path.
+ *
+ * Replaces itk::VEDMultigridImageFilter (reference include/itkVEDMultigridImageFilter.{h,hxx},
+ * cited VED.h / VED.hxx):
+ *   multiscale Hessian (ComputeHessian, VED.hxx:158-173), eigen-analysis and Frangi-type
+ *   vesselness with the per-voxel maximum over scales (UpdateVesselness / VesselnessFunction,
+ *   VED.hxx:176-299), tensor construction (GenerateDiffusionTensor, VED.hxx:302-378) and
+ *   the anisotropic-diffusion step through the MAD solver of mad.h (DiffusionStep,
+ *   VED.hxx:381-402), iterated m_Iterations times (GenerateData, VED.hxx:63-155).
+ *
+ * Everything stays on the device between stages: image (fp64, the reference's internal
+ * pixel type, VED.h:61), Hessian scratch (storage precision = desc.precision), response
+ * and vessel direction (fp64), the fp64 SoA tensor handed to the solver in place.
+ *
+ * Hessian definition (parity unpinned: ITK's HessianRecursiveGaussianImageFilter is an
+ * IIR approximation and ITK is not available to compare with): scale-normalised
+ * (sigma^2) Gaussian second derivatives by separable correlation with moment-normalised
+ * sampled Gaussian derivative kernels, radius ceil(4 sigma / h) per axis, borders
+ * replicated.  See DESIGN.md "VED tensor generation" and oracle/ved_oracle.py.
+ */
+#ifndef MAD_VED_H
+#define MAD_VED_H
+
+#include "mad.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAD_VED_MAX_SCALES 16
+
+typedef struct mad_ved_desc {
+  uint32_t abi_version;            /* MAD_ABI_VERSION */
+  int64_t size[3];                 /* x, y, z (the filter is 3D only, VED.h:46) */
+  double spacing[3];               /* image spacing (Hessian and solver), x first */
+  /* VED parameters, VED.hxx:34-58 defaults */
+  double alpha;                    /* 0.5 */
+  double beta;                     /* 0.5 */
+  double gamma;                    /* 5.0 */
+  double epsilon;                  /* 0.01 */
+  double omega;                    /* 5.0 */
+  double sensitivity;              /* 10.0 */
+  int32_t nscales;                 /* 5 */
+  double scales[MAD_VED_MAX_SCALES];/* 0.300 0.482 0.775 1.245 2.000 (physical sigma) */
+  uint32_t iterations;             /* 1  (outer VED iterations) */
+  uint32_t diffusion_iterations;   /* 5  (MAD NumberOfSteps per iteration) */
+  /* MAD parameters of DiffusionStep (VED.hxx:386-396; MaxCycles fixed at 100) */
+  int32_t cycle;                   /* MAD_VCYCLE */
+  double time_step;                /* 0.1 */
+  double tolerance;                /* 1e-6 */
+  uint32_t diffusion_iterations_per_grid; /* 2 */
+  int32_t verbose;                 /* 0 */
+  /* additions (no reference counterpart) */
+  int32_t smoother;                /* mad_smoother, default MAD_GAUSS_SEIDEL (VED.h:44) */
+  int32_t precision;               /* MAD_FP32 (default) / MAD_FP64: Hessian and solver storage */
+  int32_t device;                  /* HIP device, -1 = current */
+  int32_t reserved[8];
+} mad_ved_desc;
+
+typedef struct mad_ved_stats {
+  uint32_t iterations;             /* VED iterations run */
+  uint32_t total_cycles;           /* MAD cycles over all iterations and steps */
+  double last_relres;              /* relative residual at the end of the last step */
+  double tensor_ms;                /* device time: Hessian + vesselness + tensor, all iterations */
+  double diffusion_ms;             /* MAD setup + solve, all iterations */
+  int32_t stalled;                 /* any step ended by the fp32 stall guard */
+  int32_t reserved[7];
+} mad_ved_stats;
+
+typedef struct mad_ved_ctx mad_ved_ctx;
+
+int mad_ved_desc_init(mad_ved_desc *d);                    /* VED.hxx:34-58 defaults */
+int mad_ved_create(const mad_ved_desc *d, mad_ved_ctx **out); /* VED::New() + setters */
+void mad_ved_destroy(mad_ved_ctx *ctx);
+const char *mad_ved_last_error(const mad_ved_ctx *ctx);
+
+/* GenerateData (VED.hxx:63-155): host image in (any mad_dtype, x fastest), host image out
+ * (static_cast, i.e. truncation for integer types, VED.hxx:145). */
+int mad_ved_run(mad_ved_ctx *ctx, const void *in, int32_t in_dtype, void *out,
+                int32_t out_dtype, mad_ved_stats *stats);
+/* same with device buffers */
+int mad_ved_run_device(mad_ved_ctx *ctx, const void *in, int32_t in_dtype, void *out,
+                       int32_t out_dtype, mad_ved_stats *stats);
+
+/* One tensor generation on a host image (parity / inspection): all scales of
+ * ComputeHessian + UpdateVesselness, then GenerateDiffusionTensor.  tensor_soa: 6 arrays
+ * of N doubles [xx,xy,xz,yy,yz,zz]; response (may be NULL): N doubles, the maximum
+ * vesselness over scales. */
+int mad_ved_tensor(mad_ved_ctx *ctx, const void *image, int32_t dtype, double *tensor_soa,
+                   double *response);
+/* ComputeHessian at one scale (VED.hxx:158-173) on a host image: 6 arrays of N doubles. */
+int mad_ved_hessian(mad_ved_ctx *ctx, const void *image, int32_t dtype, double sigma,
+                    double *hessian_soa);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

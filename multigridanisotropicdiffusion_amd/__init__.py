@@ -12,11 +12,13 @@ from .filters import (Image, MultigridAnisotropicDiffusionImageFilter,
                       MultigridGaussSeidelLexSmoother, MultigridGaussSeidelSmoother,
                       MultigridWeightedJacobiSmoother, TensorImage)
 from .solver import Solver, comm_unique_id, max_depth, slab_range
+from .ved import VED, VEDMultigridImageFilter
+from . import mhd
 
 __all__ = [
     "capi", "Solver", "comm_unique_id", "max_depth", "slab_range", "Image", "TensorImage",
     "MultigridAnisotropicDiffusionImageFilter", "MultigridGaussSeidelSmoother",
     "MultigridGaussSeidelLexSmoother", "MultigridWeightedJacobiSmoother", "MadError",
     "VCYCLE", "FMG", "SMOOTHER", "GAUSS_SEIDEL", "GAUSS_SEIDEL_LEX", "WEIGHTED_JACOBI",
-    "FP32", "FP64",
+    "FP32", "FP64", "VED", "VEDMultigridImageFilter", "mhd",
 ]

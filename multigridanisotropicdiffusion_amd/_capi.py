@@ -38,7 +38,12 @@ EXPORTS = (
     "mad_synchronize", "mad_bench_smooth", "mad_smooth_kernel_name", "mad_bench_vcycle", "mad_bench_synth_tensor",
     "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_comm_init_local",
     "mad_slab_range",
+    # include/mad_ved.h
+    "mad_ved_desc_init", "mad_ved_create", "mad_ved_destroy", "mad_ved_last_error",
+    "mad_ved_run", "mad_ved_run_device", "mad_ved_tensor", "mad_ved_hessian",
 )
+
+VED_MAX_SCALES = 16
 
 
 class MadDesc(ctypes.Structure):
@@ -80,6 +85,49 @@ class MadStats(ctypes.Structure):
         ("tensor_kind", ctypes.c_int32),
         ("colors", ctypes.c_int32),
         ("reserved", ctypes.c_int32 * 5),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+class VedDesc(ctypes.Structure):
+    """mad_ved_desc (include/mad_ved.h)."""
+    _fields_ = [
+        ("abi_version", ctypes.c_uint32),
+        ("size", ctypes.c_int64 * 3),
+        ("spacing", ctypes.c_double * 3),
+        ("alpha", ctypes.c_double),
+        ("beta", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("epsilon", ctypes.c_double),
+        ("omega", ctypes.c_double),
+        ("sensitivity", ctypes.c_double),
+        ("nscales", ctypes.c_int32),
+        ("scales", ctypes.c_double * VED_MAX_SCALES),
+        ("iterations", ctypes.c_uint32),
+        ("diffusion_iterations", ctypes.c_uint32),
+        ("cycle", ctypes.c_int32),
+        ("time_step", ctypes.c_double),
+        ("tolerance", ctypes.c_double),
+        ("diffusion_iterations_per_grid", ctypes.c_uint32),
+        ("verbose", ctypes.c_int32),
+        ("smoother", ctypes.c_int32),
+        ("precision", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 8),
+    ]
+
+
+class VedStats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_uint32),
+        ("total_cycles", ctypes.c_uint32),
+        ("last_relres", ctypes.c_double),
+        ("tensor_ms", ctypes.c_double),
+        ("diffusion_ms", ctypes.c_double),
+        ("stalled", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
     ]
 
     def as_dict(self):
@@ -151,6 +199,14 @@ def load():
         "mad_comm_init": ([vp, vp], i32),
         "mad_comm_init_local": ([vp, ctypes.c_uint64], i32),
         "mad_slab_range": ([i64, i32, i32, i32, i64p, i64p], i32),
+        "mad_ved_desc_init": ([ctypes.POINTER(VedDesc)], i32),
+        "mad_ved_create": ([ctypes.POINTER(VedDesc), ctypes.POINTER(vp)], i32),
+        "mad_ved_destroy": ([vp], None),
+        "mad_ved_last_error": ([vp], ctypes.c_char_p),
+        "mad_ved_run": ([vp, vp, i32, vp, i32, ctypes.POINTER(VedStats)], i32),
+        "mad_ved_run_device": ([vp, vp, i32, vp, i32, ctypes.POINTER(VedStats)], i32),
+        "mad_ved_tensor": ([vp, vp, i32, dp, dp], i32),
+        "mad_ved_hessian": ([vp, vp, i32, dbl, dp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -11,7 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmad_hip.so")
 SOURCES = ["mad_solver.hip"]
-DEPS = ["mad_solver.hip", "mad_kernels.hpp", "mad_comm.hpp", "../../include/mad.h"]
+DEPS = ["mad_solver.hip", "mad_kernels.hpp", "mad_comm.hpp", "mad_ved.hpp", "mad_ved_kernels.hpp",
+        "../../include/mad.h", "../../include/mad_ved.h"]
 
 
 def hipcc():

@@ -77,6 +77,42 @@ inline unsigned flat_blocks(int64_t n, unsigned cap = 4096) {
 
 const dim3 BLK(64, 4, 1);
 
+// image casts (MAD.hxx:110-127 in, :270-282 static_cast out) on a stream
+template <typename T>
+void convert_to(const void* src, int dt, T* dst, int64_t n, hipStream_t stream) {
+  const unsigned nb = flat_blocks(n);
+  switch (dt) {
+    case MAD_U8: hipLaunchKernelGGL((convert_k<uint8_t, T>), dim3(nb), dim3(256), 0, stream, (const uint8_t*)src, dst, n); break;
+    case MAD_I8: hipLaunchKernelGGL((convert_k<int8_t, T>), dim3(nb), dim3(256), 0, stream, (const int8_t*)src, dst, n); break;
+    case MAD_U16: hipLaunchKernelGGL((convert_k<uint16_t, T>), dim3(nb), dim3(256), 0, stream, (const uint16_t*)src, dst, n); break;
+    case MAD_I16: hipLaunchKernelGGL((convert_k<int16_t, T>), dim3(nb), dim3(256), 0, stream, (const int16_t*)src, dst, n); break;
+    case MAD_U32: hipLaunchKernelGGL((convert_k<uint32_t, T>), dim3(nb), dim3(256), 0, stream, (const uint32_t*)src, dst, n); break;
+    case MAD_I32: hipLaunchKernelGGL((convert_k<int32_t, T>), dim3(nb), dim3(256), 0, stream, (const int32_t*)src, dst, n); break;
+    case MAD_F32: hipLaunchKernelGGL((convert_k<float, T>), dim3(nb), dim3(256), 0, stream, (const float*)src, dst, n); break;
+    case MAD_F64: hipLaunchKernelGGL((convert_k<double, T>), dim3(nb), dim3(256), 0, stream, (const double*)src, dst, n); break;
+    default: throw MadError(MAD_ERR_INVALID, "unknown input dtype");
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void convert_from(const T* src, void* dst, int dt, int64_t n, hipStream_t stream) {
+  const unsigned nb = flat_blocks(n);
+  switch (dt) {
+    case MAD_U8: hipLaunchKernelGGL((convert_int_k<T, uint8_t>), dim3(nb), dim3(256), 0, stream, src, (uint8_t*)dst, n, 0.0, 255.0); break;
+    case MAD_I8: hipLaunchKernelGGL((convert_int_k<T, int8_t>), dim3(nb), dim3(256), 0, stream, src, (int8_t*)dst, n, -128.0, 127.0); break;
+    case MAD_U16: hipLaunchKernelGGL((convert_int_k<T, uint16_t>), dim3(nb), dim3(256), 0, stream, src, (uint16_t*)dst, n, 0.0, 65535.0); break;
+    case MAD_I16: hipLaunchKernelGGL((convert_int_k<T, int16_t>), dim3(nb), dim3(256), 0, stream, src, (int16_t*)dst, n, -32768.0, 32767.0); break;
+    case MAD_U32: hipLaunchKernelGGL((convert_int_k<T, uint32_t>), dim3(nb), dim3(256), 0, stream, src, (uint32_t*)dst, n, 0.0, 4294967295.0); break;
+    case MAD_I32: hipLaunchKernelGGL((convert_int_k<T, int32_t>), dim3(nb), dim3(256), 0, stream, src, (int32_t*)dst, n, -2147483648.0, 2147483647.0); break;
+    case MAD_F32: hipLaunchKernelGGL((convert_k<T, float>), dim3(nb), dim3(256), 0, stream, src, (float*)dst, n); break;
+    case MAD_F64: hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, stream, src, (double*)dst, n); break;
+    default: throw MadError(MAD_ERR_INVALID, "unknown output dtype");
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+
 // dispatch (dim, kind) to compile-time parameters
 template <typename F>
 void dispatch(int dim, int kind, F&& f) {
@@ -1213,37 +1249,8 @@ class Solver final : public SolverBase {
   }
   double* scratch64(int64_t n) { return (double*)scratch_bytes(sizeof(double) * n); }
 
-  void convert_in(const void* src, int dt, T* dst, int64_t n) {
-    const unsigned nb = flat_blocks(n);
-    switch (dt) {
-      case MAD_U8: hipLaunchKernelGGL((convert_k<uint8_t, T>), dim3(nb), dim3(256), 0, c_->stream, (const uint8_t*)src, dst, n); break;
-      case MAD_I8: hipLaunchKernelGGL((convert_k<int8_t, T>), dim3(nb), dim3(256), 0, c_->stream, (const int8_t*)src, dst, n); break;
-      case MAD_U16: hipLaunchKernelGGL((convert_k<uint16_t, T>), dim3(nb), dim3(256), 0, c_->stream, (const uint16_t*)src, dst, n); break;
-      case MAD_I16: hipLaunchKernelGGL((convert_k<int16_t, T>), dim3(nb), dim3(256), 0, c_->stream, (const int16_t*)src, dst, n); break;
-      case MAD_U32: hipLaunchKernelGGL((convert_k<uint32_t, T>), dim3(nb), dim3(256), 0, c_->stream, (const uint32_t*)src, dst, n); break;
-      case MAD_I32: hipLaunchKernelGGL((convert_k<int32_t, T>), dim3(nb), dim3(256), 0, c_->stream, (const int32_t*)src, dst, n); break;
-      case MAD_F32: hipLaunchKernelGGL((convert_k<float, T>), dim3(nb), dim3(256), 0, c_->stream, (const float*)src, dst, n); break;
-      case MAD_F64: hipLaunchKernelGGL((convert_k<double, T>), dim3(nb), dim3(256), 0, c_->stream, (const double*)src, dst, n); break;
-      default: throw MadError(MAD_ERR_INVALID, "unknown input dtype");
-    }
-    HIP_CHECK(hipGetLastError());
-  }
-
-  void convert_out(const T* src, void* dst, int dt, int64_t n) {
-    const unsigned nb = flat_blocks(n);
-    switch (dt) {
-      case MAD_U8: hipLaunchKernelGGL((convert_int_k<T, uint8_t>), dim3(nb), dim3(256), 0, c_->stream, src, (uint8_t*)dst, n, 0.0, 255.0); break;
-      case MAD_I8: hipLaunchKernelGGL((convert_int_k<T, int8_t>), dim3(nb), dim3(256), 0, c_->stream, src, (int8_t*)dst, n, -128.0, 127.0); break;
-      case MAD_U16: hipLaunchKernelGGL((convert_int_k<T, uint16_t>), dim3(nb), dim3(256), 0, c_->stream, src, (uint16_t*)dst, n, 0.0, 65535.0); break;
-      case MAD_I16: hipLaunchKernelGGL((convert_int_k<T, int16_t>), dim3(nb), dim3(256), 0, c_->stream, src, (int16_t*)dst, n, -32768.0, 32767.0); break;
-      case MAD_U32: hipLaunchKernelGGL((convert_int_k<T, uint32_t>), dim3(nb), dim3(256), 0, c_->stream, src, (uint32_t*)dst, n, 0.0, 4294967295.0); break;
-      case MAD_I32: hipLaunchKernelGGL((convert_int_k<T, int32_t>), dim3(nb), dim3(256), 0, c_->stream, src, (int32_t*)dst, n, -2147483648.0, 2147483647.0); break;
-      case MAD_F32: hipLaunchKernelGGL((convert_k<T, float>), dim3(nb), dim3(256), 0, c_->stream, src, (float*)dst, n); break;
-      case MAD_F64: hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, c_->stream, src, (double*)dst, n); break;
-      default: throw MadError(MAD_ERR_INVALID, "unknown output dtype");
-    }
-    HIP_CHECK(hipGetLastError());
-  }
+  void convert_in(const void* src, int dt, T* dst, int64_t n) { convert_to(src, dt, dst, n, c_->stream); }
+  void convert_out(const T* src, void* dst, int dt, int64_t n) { convert_from(src, dst, dt, n, c_->stream); }
 
   // GH.hxx:110-201: level-0 DCA from the input tensor, then per level: restrict
   // every tensor component (coarse centring) and rediscretise.  Done on the full
@@ -1978,3 +1985,6 @@ int mad_comm_init_local(mad_ctx* c, uint64_t group) {
 }
 
 }  // extern "C"
+
+// VED pipeline (include/mad_ved.h): the caller of the hot path, same library
+#include "mad_ved.hpp"

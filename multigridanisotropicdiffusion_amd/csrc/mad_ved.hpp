@@ -1,0 +1,357 @@
+// mad_ved.hpp -- host driver + C ABI of include/mad_ved.h (VED pipeline on the GPU).
+// Included at the end of mad_solver.hip: it drives the MAD solver through its
+// internal entry points (the same ones mad_run uses), no host round trips between
+// the tensor generation and the diffusion step.
+//
+// Reference: include/itkVEDMultigridImageFilter.{h,hxx} (VED.h / VED.hxx).
+#include "../../include/mad_ved.h"
+#include "mad_ved_kernels.hpp"
+
+struct mad_ved_ctx {
+  mad_ved_desc d{};
+  std::string err;
+  mad_ctx* mad = nullptr;  // the DiffusionStep filter (VED.hxx:386-398), kept across iterations
+  int64_t n[3] = {0, 0, 0};
+  int64_t N = 0;
+  double* img = nullptr;   // internal image (fp64, VED.h:61)
+  double* img2 = nullptr;  // next iterate
+  void* fir = nullptr;     // 9 FIR volumes in the storage precision
+  void* taps = nullptr;    // per-axis taps of the current scale (device)
+  double* resp = nullptr;  // m_MaxVesselnessResponse
+  double* dir = nullptr;   // vessel direction (eigenvector column 2 of the max scale), SoA x3
+  void* stage = nullptr;   // host <-> device staging
+  size_t stage_bytes = 0;
+  ~mad_ved_ctx() {
+    if (mad) (void)hipSetDevice(mad->device);
+    if (mad && mad->stream) (void)hipStreamSynchronize(mad->stream);
+    for (void* p : {(void*)img, (void*)img2, fir, taps, (void*)resp, (void*)dir, stage})
+      if (p) (void)hipFree(p);
+    if (mad) mad_destroy(mad);
+  }
+};
+
+namespace {
+
+template <typename F>
+int ved_guarded(mad_ved_ctx* v, F&& f) {
+  try {
+    f();
+    return MAD_OK;
+  } catch (const MadError& e) {
+    g_last_error = e.what();
+    if (v) v->err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "out of host memory";
+    if (v) v->err = g_last_error;
+    return MAD_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    if (v) v->err = e.what();
+    return MAD_ERR_DEVICE;
+  }
+}
+
+// MAD call inside a VED call: forward its status and message
+void mad_call(mad_ctx* c, int rc) {
+  if (rc != MAD_OK) throw MadError(rc, "diffusion step: " + c->err);
+}
+
+// Gaussian derivative taps for one axis: [K0 | K1 | K2], R = ceil(4 sigma / h)
+// (oracle/ved_oracle.py gauss_kernels restates the same definition):
+//   K0 = g / S0,  K1 = t g / S2,  K2 = a (t^2 - m) g,  m = S2 / S0,  a = 2 / (S4 - m S2)
+int ved_taps(double sigma, double h, std::vector<double>& K) {
+  const int R = std::max(1, (int)std::ceil(4.0 * sigma / h));
+  const double s = sigma / h;
+  const int W = 2 * R + 1;
+  std::vector<double> g(W), t(W);
+  double S0 = 0.0, S2 = 0.0, S4 = 0.0;
+  for (int q = 0; q < W; ++q) {
+    t[q] = (double)(q - R);
+    g[q] = std::exp(-(t[q] * t[q]) / (2.0 * s * s));
+  }
+  for (int q = 0; q < W; ++q) {
+    S0 += g[q];
+    S2 += t[q] * t[q] * g[q];
+    S4 += t[q] * t[q] * t[q] * t[q] * g[q];
+  }
+  const double m = S2 / S0;
+  const double a = 2.0 / (S4 - m * S2);
+  K.assign(3 * W, 0.0);
+  for (int q = 0; q < W; ++q) {
+    K[q] = g[q] / S0;
+    K[W + q] = t[q] * g[q] / S2;
+    K[2 * W + q] = a * (t[q] * t[q] - m) * g[q];
+  }
+  return R;
+}
+
+void* ved_stage(mad_ved_ctx* v, size_t bytes) {
+  if (bytes > v->stage_bytes) {
+    if (v->stage) HIP_CHECK(hipFree(v->stage));
+    v->stage = nullptr;
+    HIP_CHECK(hipMalloc(&v->stage, bytes));
+    v->stage_bytes = bytes;
+  }
+  return v->stage;
+}
+
+// device image (any dtype) -> v->img (fp64)
+void ved_load_image(mad_ved_ctx* v, const void* src, int dt, bool dev) {
+  const size_t es = dtype_size(dt);
+  REQUIRE(es, MAD_ERR_INVALID, "bad image dtype");
+  hipStream_t st = v->mad->stream;
+  if (!dev) {
+    void* s = ved_stage(v, es * v->N);
+    HIP_CHECK(hipMemcpyAsync(s, src, es * v->N, hipMemcpyHostToDevice, st));
+    src = s;
+  }
+  convert_to<double>(src, dt, v->img, v->N, st);
+}
+
+// one scale: Hessian (MODE VED_HESSIAN, into `hess`) or vesselness update
+template <typename T>
+void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess) {
+  hipStream_t st = v->mad->stream;
+  const int nx = (int)v->n[0], ny = (int)v->n[1], nz = (int)v->n[2];
+  const int64_t N = v->N;
+  if (!v->fir) HIP_CHECK(hipMalloc(&v->fir, sizeof(T) * 9 * N));
+  T* f = (T*)v->fir;
+  T *z0 = f, *z1 = f + N, *z2 = f + 2 * N;
+  T *a00 = f + 3 * N, *a10 = f + 4 * N, *a20 = f + 5 * N, *a01 = f + 6 * N, *a11 = f + 7 * N,
+    *a02 = f + 8 * N;
+  std::vector<double> K[3];
+  int R[3];
+  for (int q = 0; q < 3; ++q) R[q] = ved_taps(sigma, v->d.spacing[q], K[q]);
+  const size_t W[3] = {K[0].size(), K[1].size(), K[2].size()};
+  std::vector<T> kt;
+  for (int q = 0; q < 3; ++q)
+    for (double x : K[q]) kt.push_back((T)x);
+  if (v->taps) HIP_CHECK(hipFree(v->taps));
+  v->taps = nullptr;
+  HIP_CHECK(hipMalloc(&v->taps, sizeof(T) * kt.size()));
+  HIP_CHECK(hipMemcpyAsync(v->taps, kt.data(), sizeof(T) * kt.size(), hipMemcpyHostToDevice, st));
+  const T* tx = (const T*)v->taps;
+  const T* ty = tx + W[0];
+  const T* tz = ty + W[1];
+  const dim3 gr = grid_for(nx, ny, nz, BLK);
+  hipLaunchKernelGGL((ved_fir_z_k<T>), gr, BLK, 0, st, v->img, z0, z1, z2, tz, R[2], nx, ny, nz);
+  hipLaunchKernelGGL((ved_fir_y_k<T>), gr, BLK, 0, st, z0, z1, z2, a00, a10, a20, a01, a11, a02,
+                     ty, R[1], nx, ny, nz);
+  HessScale hs;
+  const double s2 = sigma * sigma, *h = v->d.spacing;
+  const int cd[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+  for (int c = 0; c < 6; ++c) hs.f[c] = s2 / (h[cd[c][0]] * h[cd[c][1]]);
+  const VesselParams vp{v->d.alpha, v->d.beta, v->d.gamma};
+  if (mode == VED_HESSIAN)
+    hipLaunchKernelGGL((ved_fir_x_k<T, VED_HESSIAN>), gr, BLK, 0, st, a00, a10, a20, a01, a11, a02,
+                       tx, R[0], nx, ny, nz, hs, hess, nullptr, nullptr, 0, vp);
+  else
+    hipLaunchKernelGGL((ved_fir_x_k<T, VED_UPDATE>), gr, BLK, 0, st, a00, a10, a20, a01, a11, a02,
+                       tx, R[0], nx, ny, nz, hs, nullptr, v->resp, v->dir, first ? 1 : 0, vp);
+  HIP_CHECK(hipGetLastError());
+  // the host tap vector dies here: the copy must have landed
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
+// ComputeHessian + UpdateVesselness over all scales, GenerateDiffusionTensor into the
+// solver's fp64 tensor (VED.hxx:109-120)
+template <typename T>
+void ved_tensor_impl(mad_ved_ctx* v) {
+  mad_ctx* c = v->mad;
+  const int64_t N = v->N;
+  if (!v->resp) HIP_CHECK(hipMalloc(&v->resp, sizeof(double) * N));
+  if (!v->dir) HIP_CHECK(hipMalloc(&v->dir, sizeof(double) * 3 * N));
+  for (int s = 0; s < v->d.nscales; ++s) ved_scale<T>(v, v->d.scales[s], VED_UPDATE, s == 0, nullptr);
+  if (!c->tensor64) HIP_CHECK(hipMalloc(&c->tensor64, sizeof(double) * 6 * N));
+  hipLaunchKernelGGL(ved_tensor_k, dim3(flat_blocks(N)), dim3(256), 0, c->stream, v->resp, v->dir,
+                     c->tensor64, N, v->d.epsilon, v->d.omega, v->d.sensitivity);
+  HIP_CHECK(hipGetLastError());
+  c->tensor_set = true;
+  c->setup_done = false;  // DiffusionStep builds a new filter per iteration (VED.hxx:386)
+}
+
+void ved_tensor_any(mad_ved_ctx* v) {
+  if (v->d.precision == MAD_FP64) ved_tensor_impl<double>(v);
+  else ved_tensor_impl<float>(v);
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+// GenerateData (VED.hxx:63-155)
+void ved_run_impl(mad_ved_ctx* v, const void* in, int in_dt, void* out, int out_dt, bool dev,
+                  mad_ved_stats* st) {
+  mad_ctx* c = v->mad;
+  HIP_CHECK(hipSetDevice(c->device));
+  const size_t oes = dtype_size(out_dt);
+  REQUIRE(oes, MAD_ERR_INVALID, "bad output dtype");
+  ved_load_image(v, in, in_dt, dev);
+  hipEvent_t ev[4];
+  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  double tensor_ms = 0.0, diff_ms = 0.0, relres = 0.0;
+  unsigned cycles = 0;
+  int stalled = 0;
+  for (uint32_t it = 0; it < v->d.iterations; ++it) {  // VED.hxx:104
+    if (v->d.verbose) std::printf("Iteration n.%u...\n", it + 1);
+    HIP_CHECK(hipEventRecord(ev[0], c->stream));
+    ved_tensor_any(v);
+    HIP_CHECK(hipEventRecord(ev[1], c->stream));
+    mad_stats ms{};
+    mad_call(c, run_impl(c, v->img, MAD_F64, v->img2, MAD_F64, &ms, true));  // DiffusionStep
+    HIP_CHECK(hipEventRecord(ev[2], c->stream));
+    HIP_CHECK(hipEventSynchronize(ev[2]));
+    tensor_ms += elapsed(ev[0], ev[1]);
+    diff_ms += elapsed(ev[1], ev[2]);
+    std::swap(v->img, v->img2);
+    cycles += ms.total_cycles;
+    relres = ms.last_relres;
+    stalled |= ms.stalled;
+  }
+  for (auto& e : ev) HIP_CHECK(hipEventDestroy(e));
+  // static_cast to the output pixel type (VED.hxx:139-150)
+  void* dst = dev ? out : ved_stage(v, oes * v->N);
+  convert_from<double>(v->img, dst, out_dt, v->N, c->stream);
+  if (!dev) HIP_CHECK(hipMemcpyAsync(out, dst, oes * v->N, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->iterations = v->d.iterations;
+    st->total_cycles = cycles;
+    st->last_relres = relres;
+    st->tensor_ms = tensor_ms;
+    st->diffusion_ms = diff_ms;
+    st->stalled = stalled;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mad_ved_desc_init(mad_ved_desc* d) {
+  if (!d) return MAD_ERR_INVALID;
+  std::memset(d, 0, sizeof(*d));
+  d->abi_version = MAD_ABI_VERSION;
+  d->size[0] = d->size[1] = d->size[2] = 1;
+  d->spacing[0] = d->spacing[1] = d->spacing[2] = 1.0;
+  d->alpha = 0.5;        // VED.hxx:36
+  d->beta = 0.5;         // :37
+  d->gamma = 5.0;        // :38
+  d->epsilon = 0.01;     // :39
+  d->omega = 5.0;        // :40
+  d->sensitivity = 10.0; // :41
+  d->iterations = 1;     // :42
+  d->diffusion_iterations = 5;  // :43
+  d->cycle = MAD_VCYCLE; // :44
+  d->time_step = 0.1;    // :45
+  d->tolerance = 1e-6;   // :46
+  d->diffusion_iterations_per_grid = 2;  // :47
+  d->nscales = 5;        // :52-58
+  const double sc[5] = {0.300, 0.482, 0.775, 1.245, 2.000};
+  for (int q = 0; q < 5; ++q) d->scales[q] = sc[q];
+  d->smoother = MAD_GAUSS_SEIDEL;
+  d->precision = MAD_FP32;
+  d->device = -1;
+  return MAD_OK;
+}
+
+int mad_ved_create(const mad_ved_desc* d, mad_ved_ctx** out) {
+  if (!out) return MAD_ERR_INVALID;
+  *out = nullptr;
+  std::unique_ptr<mad_ved_ctx> v(new mad_ved_ctx());
+  int rc = ved_guarded(nullptr, [&] {
+    REQUIRE(d, MAD_ERR_INVALID, "null descriptor");
+    REQUIRE(d->abi_version == MAD_ABI_VERSION, MAD_ERR_INVALID, "ABI version mismatch");
+    REQUIRE(d->nscales >= 1 && d->nscales <= MAD_VED_MAX_SCALES, MAD_ERR_INVALID,
+            "nscales must be 1.." + std::to_string(MAD_VED_MAX_SCALES));
+    for (int s = 0; s < d->nscales; ++s)
+      REQUIRE(d->scales[s] > 0.0, MAD_ERR_INVALID, "scales must be positive");
+    REQUIRE(d->sensitivity != 0.0, MAD_ERR_INVALID, "sensitivity must be nonzero");
+    v->d = *d;
+    mad_desc md;
+    mad_desc_init(&md);
+    md.dim = 3;
+    for (int q = 0; q < 3; ++q) {
+      md.size[q] = d->size[q];
+      md.spacing[q] = d->spacing[q];
+    }
+    md.cycle = d->cycle;
+    md.smoother = d->smoother;
+    md.iterations_per_grid = d->diffusion_iterations_per_grid;
+    md.max_cycles = 100;  // VED.hxx:396
+    md.number_of_steps = d->diffusion_iterations;
+    md.time_step = d->time_step;
+    md.tolerance = d->tolerance;
+    md.verbose = d->verbose;
+    md.precision = d->precision;
+    md.device = d->device;
+    const int mrc = mad_create(&md, &v->mad);
+    if (mrc != MAD_OK) throw MadError(mrc, g_last_error);
+    for (int q = 0; q < 3; ++q) v->n[q] = d->size[q];
+    v->N = v->n[0] * v->n[1] * v->n[2];
+    REQUIRE(v->n[0] <= INT32_MAX && v->n[1] <= INT32_MAX && v->n[2] <= 65535, MAD_ERR_INVALID,
+            "image too large for the VED grid mapping");
+    HIP_CHECK(hipSetDevice(v->mad->device));
+    HIP_CHECK(hipMalloc(&v->img, sizeof(double) * v->N));
+    HIP_CHECK(hipMalloc(&v->img2, sizeof(double) * v->N));
+  });
+  if (rc != MAD_OK) return rc;
+  *out = v.release();
+  return MAD_OK;
+}
+
+void mad_ved_destroy(mad_ved_ctx* v) { delete v; }
+
+const char* mad_ved_last_error(const mad_ved_ctx* v) { return v ? v->err.c_str() : g_last_error.c_str(); }
+
+int mad_ved_run(mad_ved_ctx* v, const void* in, int32_t in_dtype, void* out, int32_t out_dtype,
+                mad_ved_stats* st) {
+  if (!v || !in || !out) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, false, st); });
+}
+
+int mad_ved_run_device(mad_ved_ctx* v, const void* in, int32_t in_dtype, void* out,
+                       int32_t out_dtype, mad_ved_stats* st) {
+  if (!v || !in || !out) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, true, st); });
+}
+
+int mad_ved_tensor(mad_ved_ctx* v, const void* image, int32_t dtype, double* tensor_soa,
+                   double* response) {
+  if (!v || !image || !tensor_soa) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] {
+    HIP_CHECK(hipSetDevice(v->mad->device));
+    ved_load_image(v, image, dtype, false);
+    ved_tensor_any(v);
+    hipStream_t st = v->mad->stream;
+    HIP_CHECK(hipMemcpyAsync(tensor_soa, v->mad->tensor64, sizeof(double) * 6 * v->N,
+                             hipMemcpyDeviceToHost, st));
+    if (response)
+      HIP_CHECK(hipMemcpyAsync(response, v->resp, sizeof(double) * v->N, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+
+int mad_ved_hessian(mad_ved_ctx* v, const void* image, int32_t dtype, double sigma,
+                    double* hessian_soa) {
+  if (!v || !image || !hessian_soa) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] {
+    REQUIRE(sigma > 0.0, MAD_ERR_INVALID, "sigma must be positive");
+    HIP_CHECK(hipSetDevice(v->mad->device));
+    ved_load_image(v, image, dtype, false);
+    double* H = nullptr;
+    HIP_CHECK(hipMalloc(&H, sizeof(double) * 6 * v->N));
+    if (v->d.precision == MAD_FP64) ved_scale<double>(v, sigma, VED_HESSIAN, true, H);
+    else ved_scale<float>(v, sigma, VED_HESSIAN, true, H);
+    HIP_CHECK(hipMemcpyAsync(hessian_soa, H, sizeof(double) * 6 * v->N, hipMemcpyDeviceToHost,
+                             v->mad->stream));
+    HIP_CHECK(hipStreamSynchronize(v->mad->stream));
+    HIP_CHECK(hipFree(H));
+  });
+}
+
+}  // extern "C"

@@ -1,5 +1,5 @@
 """C ABI checks that need no GPU: the library loads, exports every symbol
-include/mad.h declares, validates descriptors, and plans the hierarchy /
+include/mad.h and include/mad_ved.h declare, validates descriptors, and plans the hierarchy /
 z-slab decomposition identically to the oracle's depth rule."""
 import ctypes
 import os
@@ -15,9 +15,13 @@ from conftest import ROOT
 
 
 def header_functions():
-    src = open(os.path.join(ROOT, "include", "mad.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(mad_[a-z0-9_]+)\s*\(", src)))
+    """Every function declared by the C headers (include/mad.h, include/mad_ved.h)."""
+    names = set()
+    for h in ("mad.h", "mad_ved.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(mad_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_header_symbol():

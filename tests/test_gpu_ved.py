@@ -1,0 +1,126 @@
+"""VED pipeline on the GPU (include/mad_ved.h) against the fp64 oracle
+(oracle/ved_oracle.py + the C MAD oracle).
+
+Tolerances (written per test):
+  Hessian: fp64 storage <= 1e-12 of max|H|; fp32 storage <= 2e-6 of max|H|.
+  Tensor / response (fp64 eigen-analysis on the fp64 Hessian): <= 1e-9 absolute
+    (Jacobi rotations vs LAPACK: rounding-level differences only).
+  Whole filter on the reference's own test volume and parameters (itkVEDTest_GS.cxx):
+    ||u_gpu - u_ref||_inf / ||u_ref||_inf <= 1e-5 (fp32, north-star bar), <= 1e-8 (fp64);
+    short output: truncation of the same values, |diff| <= 1.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import ved_oracle as VO
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+SP = (0.3125, 0.3125, 0.5)  # ved_test spacing (x, y, z)
+
+
+@pytest.fixture(scope="module")
+def M():
+    import multigridanisotropicdiffusion_amd as mod
+    return mod
+
+
+@pytest.fixture(scope="module")
+def ved_volume():
+    from multigridanisotropicdiffusion_amd import mhd
+    arr, info = mhd.read_mhd(os.path.join(GOLDEN, "ved_test.mhd"))
+    return arr, tuple(info["spacing"])
+
+
+VED_TEST_KW = dict(alpha=0.5, beta=0.5, gamma=5.0, epsilon=0.01, sensitivity=10.0, omega=1.5,
+                   iterations=1, diffusion_iterations=4, diffusion_iterations_per_grid=3,
+                   time_step=0.1, tolerance=1e-10)
+
+
+@pytest.fixture(scope="module")
+def ved_ref(oracle_mod, ved_volume):
+    img, sp = ved_volume
+    return VO.ved_run(img, sp, oracle_mod, **VED_TEST_KW)
+
+
+def relmax(a, ref):
+    return np.abs(a - ref).max() / np.abs(ref).max()
+
+
+@pytest.mark.parametrize("precision,tol", [("FP64", 1e-12), ("FP32", 2e-6)])
+@pytest.mark.parametrize("sigma", [0.3, 0.775, 2.0])
+def test_hessian_matches_oracle(M, precision, tol, sigma):
+    rng = np.random.default_rng(11)
+    shape = (22, 26, 30)
+    img = rng.normal(50.0, 20.0, size=shape)
+    v = M.VED(shape, SP, precision=getattr(M, precision))
+    H = v.hessian(img, sigma)
+    ref = VO.hessian(img, SP, sigma)
+    for q in range(6):
+        assert relmax(H[q], ref[..., q]) < tol, q
+
+
+def test_tensor_matches_oracle_on_reference_crop(M):
+    crop = np.load(os.path.join(GOLDEN, "ved_crop_i16.npy"))
+    v = M.VED(crop.shape, SP, omega=1.5, precision=M.FP64)
+    T, resp = v.tensor(crop)
+    Tr, rr = VO.ved_tensor(crop.astype(np.float64), SP, omega=1.5)
+    assert np.abs(resp - rr).max() < 1e-9
+    assert ((resp > 0) == (rr > 0)).mean() > 0.999
+    assert np.abs(T - Tr).max() < 1e-6
+
+
+def test_tensor_fp32_hessian_close_to_oracle(M):
+    crop = np.load(os.path.join(GOLDEN, "ved_crop_i16.npy"))
+    v = M.VED(crop.shape, SP, omega=1.5, precision=M.FP32)
+    T, resp = v.tensor(crop)
+    Tr, rr = VO.ved_tensor(crop.astype(np.float64), SP, omega=1.5)
+    assert np.abs(resp - rr).max() < 1e-4
+    # V = resp^(1/10) amplifies tiny responses; the tensor stays within 1e-3
+    assert np.abs(T - Tr).max() < 1e-3
+
+
+@pytest.mark.parametrize("precision,tol", [("FP32", 1e-5), ("FP64", 1e-8)])
+def test_ved_filter_on_reference_test_volume(M, ved_volume, ved_ref, precision, tol):
+    """itkVEDTest_GS parameters: scales .3 .482 .775 1.245 2, alpha .5, beta .5,
+    gamma 5, epsilon .01, sensitivity 10, omega 1.5, 1 iteration, 4 diffusion steps,
+    3 iterations per grid, dt 0.1, tolerance 1e-10, V-cycle, short in / out."""
+    img, sp = ved_volume
+    ref, _ = ved_ref
+    v = M.VED(img.shape, sp, precision=getattr(M, precision), **VED_TEST_KW)
+    out, st = v.run(img, out_dtype=np.float64)
+    assert st["iterations"] == 1 and st["total_cycles"] >= 4
+    assert relmax(out, ref) < tol
+    out16, _ = v.run(img, out_dtype=np.int16)
+    assert np.abs(out16.astype(np.float64) - np.trunc(ref)).max() <= 1
+
+
+def test_ved_filter_facade_and_iterations(M):
+    """Two VED iterations through the ITK-shaped facade: the output pixel type follows
+    the input (short), spacing and origin carry over."""
+    crop = np.load(os.path.join(GOLDEN, "ved_crop_i16.npy"))
+    f = M.VEDMultigridImageFilter()
+    f.SetInput(M.Image(crop, spacing=SP, origin=(1.0, 2.0, 3.0)))
+    f.SetIterations(2)
+    f.SetDiffusionIterations(2)
+    f.SetOmega(1.5)
+    f.SetTolerance(1e-8)
+    out = f.Update()
+    assert out.GetBufferAsArray().dtype == np.int16 and out.GetBufferAsArray().shape == crop.shape
+    assert out.spacing == SP and out.origin == (1.0, 2.0, 3.0)
+    assert f.stats["iterations"] == 2
+    # diffusion smooths: the output's variance is below the input's
+    assert out.GetBufferAsArray().astype(float).std() < crop.astype(float).std()
+
+
+def test_constant_volume_is_a_fixed_point(M):
+    shape = (20, 22, 24)
+    v = M.VED(shape, (1.0, 1.0, 1.0), omega=1.5, diffusion_iterations=2)
+    out, _ = v.run(np.full(shape, 42.0), out_dtype=np.float64)
+    assert np.abs(out - 42.0).max() < 1e-4
+    T, resp = v.tensor(np.full(shape, 42.0))
+    assert resp.max() == 0.0
+    assert np.array_equal(T[0], np.ones(shape)) and np.array_equal(T[1], np.zeros(shape))
