@@ -56,7 +56,9 @@ typedef struct mad_ved_desc {
   int32_t smoother;                /* mad_smoother, default MAD_GAUSS_SEIDEL (VED.h:44) */
   int32_t precision;               /* MAD_FP32 (default) / MAD_FP64: Hessian and solver storage */
   int32_t device;                  /* HIP device, -1 = current */
-  int32_t reserved[8];
+  int32_t nranks;                  /* z-slab ranks of the diffusion step (1 = single GPU) */
+  int32_t rank;
+  int32_t reserved[6];
 } mad_ved_desc;
 
 typedef struct mad_ved_stats {
@@ -77,12 +79,21 @@ void mad_ved_destroy(mad_ved_ctx *ctx);
 const char *mad_ved_last_error(const mad_ved_ctx *ctx);
 
 /* GenerateData (VED.hxx:63-155): host image in (any mad_dtype, x fastest), host image out
- * (static_cast, i.e. truncation for integer types, VED.hxx:145). */
+ * (static_cast, i.e. truncation for integer types, VED.hxx:145).
+ * Multi-GPU (nranks > 1, after mad_ved_comm_init*): every rank passes the WHOLE image and
+ * receives ITS z-slab (mad_slab_range planes).  The tensor generation is replicated on
+ * every rank (like the solver's operator setup); the diffusion steps run on z-slabs
+ * with RCCL halos; between VED iterations the slabs are all-gathered. */
 int mad_ved_run(mad_ved_ctx *ctx, const void *in, int32_t in_dtype, void *out,
                 int32_t out_dtype, mad_ved_stats *stats);
 /* same with device buffers */
 int mad_ved_run_device(mad_ved_ctx *ctx, const void *in, int32_t in_dtype, void *out,
                        int32_t out_dtype, mad_ved_stats *stats);
+
+/* Join the ranks of a multi-GPU run (mad_comm_unique_id creates the id on rank 0);
+ * the in-process variant runs ranks as threads on one device (tests). */
+int mad_ved_comm_init(mad_ved_ctx *ctx, const void *uid128);
+int mad_ved_comm_init_local(mad_ved_ctx *ctx, uint64_t group);
 
 /* One tensor generation on a host image (parity / inspection): all scales of
  * ComputeHessian + UpdateVesselness, then GenerateDiffusionTensor.  tensor_soa: 6 arrays

@@ -40,7 +40,8 @@ EXPORTS = (
     "mad_slab_range",
     # include/mad_ved.h
     "mad_ved_desc_init", "mad_ved_create", "mad_ved_destroy", "mad_ved_last_error",
-    "mad_ved_run", "mad_ved_run_device", "mad_ved_tensor", "mad_ved_hessian",
+    "mad_ved_run", "mad_ved_run_device", "mad_ved_comm_init", "mad_ved_comm_init_local",
+    "mad_ved_tensor", "mad_ved_hessian",
 )
 
 VED_MAX_SCALES = 16
@@ -115,7 +116,9 @@ class VedDesc(ctypes.Structure):
         ("smoother", ctypes.c_int32),
         ("precision", ctypes.c_int32),
         ("device", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 8),
+        ("nranks", ctypes.c_int32),
+        ("rank", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 
@@ -205,6 +208,8 @@ def load():
         "mad_ved_last_error": ([vp], ctypes.c_char_p),
         "mad_ved_run": ([vp, vp, i32, vp, i32, ctypes.POINTER(VedStats)], i32),
         "mad_ved_run_device": ([vp, vp, i32, vp, i32, ctypes.POINTER(VedStats)], i32),
+        "mad_ved_comm_init": ([vp, vp], i32),
+        "mad_ved_comm_init_local": ([vp, ctypes.c_uint64], i32),
         "mad_ved_tensor": ([vp, vp, i32, dp, dp], i32),
         "mad_ved_hessian": ([vp, vp, i32, dbl, dp], i32),
     }

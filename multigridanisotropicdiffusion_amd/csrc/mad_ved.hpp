@@ -109,6 +109,19 @@ void ved_load_image(mad_ved_ctx* v, const void* src, int dt, bool dev) {
   convert_to<double>(src, dt, v->img, v->N, st);
 }
 
+constexpr size_t kVedLds = 128 * 1024;  // dynamic LDS cap of the FIR tiles
+
+// allow the FIR kernels more than the default 64 KiB of dynamic LDS (once per type)
+template <typename T>
+void ved_lds_attr() {
+  static bool done = false;
+  if (done) return;
+  for (const void* k : {(const void*)ved_fir_z_k<T>, (const void*)ved_fir_y_k<T>,
+                        (const void*)ved_fir_x_k<T, VED_HESSIAN>, (const void*)ved_fir_x_k<T, VED_UPDATE>})
+    HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kVedLds));
+  done = true;
+}
+
 // one scale: Hessian (MODE VED_HESSIAN, into `hess`) or vesselness update
 template <typename T>
 void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess) {
@@ -134,20 +147,32 @@ void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess)
   const T* tx = (const T*)v->taps;
   const T* ty = tx + W[0];
   const T* tz = ty + W[1];
-  const dim3 gr = grid_for(nx, ny, nz, BLK);
-  hipLaunchKernelGGL((ved_fir_z_k<T>), gr, BLK, 0, st, v->img, z0, z1, z2, tz, R[2], nx, ny, nz);
-  hipLaunchKernelGGL((ved_fir_y_k<T>), gr, BLK, 0, st, z0, z1, z2, a00, a10, a20, a01, a11, a02,
-                     ty, R[1], nx, ny, nz);
+  // LDS-staged passes: z tiles of ZT planes, y tiles of YT rows (smaller when the taps
+  // are long), x rows of 256
+  auto lds_for = [](int lines, int width, int copies) { return (size_t)lines * width * copies * sizeof(T); };
+  int ZT = 32, YT = 32;
+  while (ZT > 4 && lds_for(ZT + 2 * R[2], 256, 1) > kVedLds) ZT /= 2;
+  while (YT > 4 && lds_for(YT + 2 * R[1], 64, 3) > kVedLds) YT /= 2;
+  const size_t lz = lds_for(ZT + 2 * R[2], 256, 1), ly = lds_for(YT + 2 * R[1], 64, 3);
+  const size_t lx = lds_for(256 + 2 * R[0], 1, 6);
+  REQUIRE(lz <= kVedLds && ly <= kVedLds && lx <= kVedLds, MAD_ERR_UNSUPPORTED,
+          "Gaussian taps too long for the LDS tiles (sigma / spacing > ~18)");
+  ved_lds_attr<T>();
+  hipLaunchKernelGGL((ved_fir_z_k<T>), dim3((nx + 63) / 64, (ny + 3) / 4, (nz + ZT - 1) / ZT),
+                     dim3(256), lz, st, v->img, z0, z1, z2, tz, R[2], nx, ny, nz, ZT);
+  hipLaunchKernelGGL((ved_fir_y_k<T>), dim3((nx + 63) / 64, (ny + YT - 1) / YT, nz), dim3(256), ly,
+                     st, z0, z1, z2, a00, a10, a20, a01, a11, a02, ty, R[1], nx, ny, nz, YT);
+  const dim3 gr((nx + 255) / 256, ny, nz);
   HessScale hs;
   const double s2 = sigma * sigma, *h = v->d.spacing;
   const int cd[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
   for (int c = 0; c < 6; ++c) hs.f[c] = s2 / (h[cd[c][0]] * h[cd[c][1]]);
   const VesselParams vp{v->d.alpha, v->d.beta, v->d.gamma};
   if (mode == VED_HESSIAN)
-    hipLaunchKernelGGL((ved_fir_x_k<T, VED_HESSIAN>), gr, BLK, 0, st, a00, a10, a20, a01, a11, a02,
+    hipLaunchKernelGGL((ved_fir_x_k<T, VED_HESSIAN>), gr, dim3(256), lx, st, a00, a10, a20, a01, a11, a02,
                        tx, R[0], nx, ny, nz, hs, hess, nullptr, nullptr, 0, vp);
   else
-    hipLaunchKernelGGL((ved_fir_x_k<T, VED_UPDATE>), gr, BLK, 0, st, a00, a10, a20, a01, a11, a02,
+    hipLaunchKernelGGL((ved_fir_x_k<T, VED_UPDATE>), gr, dim3(256), lx, st, a00, a10, a20, a01, a11, a02,
                        tx, R[0], nx, ny, nz, hs, nullptr, v->resp, v->dir, first ? 1 : 0, vp);
   HIP_CHECK(hipGetLastError());
   // the host tap vector dies here: the copy must have landed
@@ -182,6 +207,16 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// this rank's z-slab of level 0: [z0, z1) planes, element offset and count
+struct VedSlab {
+  int64_t off, n;
+};
+VedSlab ved_slab(const mad_ved_ctx* v) {
+  const LevelGeom& G = v->mad->geom[0];
+  const int64_t plane = v->n[0] * v->n[1];
+  return VedSlab{G.z0 * plane, (G.z1 - G.z0) * plane};
+}
+
 // GenerateData (VED.hxx:63-155)
 void ved_run_impl(mad_ved_ctx* v, const void* in, int in_dt, void* out, int out_dt, bool dev,
                   mad_ved_stats* st) {
@@ -189,6 +224,9 @@ void ved_run_impl(mad_ved_ctx* v, const void* in, int in_dt, void* out, int out_
   HIP_CHECK(hipSetDevice(c->device));
   const size_t oes = dtype_size(out_dt);
   REQUIRE(oes, MAD_ERR_INVALID, "bad output dtype");
+  const bool dist = c->comm.active();
+  REQUIRE(dist || c->d.nranks == 1, MAD_ERR_STATE, "nranks > 1 needs mad_ved_comm_init first");
+  const VedSlab sl = ved_slab(v);
   ved_load_image(v, in, in_dt, dev);
   hipEvent_t ev[4];
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
@@ -196,26 +234,32 @@ void ved_run_impl(mad_ved_ctx* v, const void* in, int in_dt, void* out, int out_
   unsigned cycles = 0;
   int stalled = 0;
   for (uint32_t it = 0; it < v->d.iterations; ++it) {  // VED.hxx:104
-    if (v->d.verbose) std::printf("Iteration n.%u...\n", it + 1);
+    if (v->d.verbose && c->comm.rank() == 0) std::printf("Iteration n.%u...\n", it + 1);
     HIP_CHECK(hipEventRecord(ev[0], c->stream));
-    ved_tensor_any(v);
+    ved_tensor_any(v);  // whole image, every rank
     HIP_CHECK(hipEventRecord(ev[1], c->stream));
     mad_stats ms{};
-    mad_call(c, run_impl(c, v->img, MAD_F64, v->img2, MAD_F64, &ms, true));  // DiffusionStep
+    mad_call(c, run_impl(c, v->img + sl.off, MAD_F64, v->img2 + sl.off, MAD_F64, &ms, true));
+    if (dist) {
+      // the next iteration's Hessian (and the caller) see the whole new image
+      c->comm.allgather_slabs(v->img2 + sl.off, v->img, v->n[0] * v->n[1], v->n[2], sizeof(double),
+                              c->stream);
+    } else {
+      std::swap(v->img, v->img2);
+    }
     HIP_CHECK(hipEventRecord(ev[2], c->stream));
     HIP_CHECK(hipEventSynchronize(ev[2]));
     tensor_ms += elapsed(ev[0], ev[1]);
     diff_ms += elapsed(ev[1], ev[2]);
-    std::swap(v->img, v->img2);
     cycles += ms.total_cycles;
     relres = ms.last_relres;
     stalled |= ms.stalled;
   }
   for (auto& e : ev) HIP_CHECK(hipEventDestroy(e));
-  // static_cast to the output pixel type (VED.hxx:139-150)
-  void* dst = dev ? out : ved_stage(v, oes * v->N);
-  convert_from<double>(v->img, dst, out_dt, v->N, c->stream);
-  if (!dev) HIP_CHECK(hipMemcpyAsync(out, dst, oes * v->N, hipMemcpyDeviceToHost, c->stream));
+  // static_cast of this rank's slab to the output pixel type (VED.hxx:139-150)
+  void* dst = dev ? out : ved_stage(v, oes * sl.n);
+  convert_from<double>(v->img + sl.off, dst, out_dt, sl.n, c->stream);
+  if (!dev) HIP_CHECK(hipMemcpyAsync(out, dst, oes * sl.n, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(hipStreamSynchronize(c->stream));
   if (st) {
     std::memset(st, 0, sizeof(*st));
@@ -256,6 +300,8 @@ int mad_ved_desc_init(mad_ved_desc* d) {
   d->smoother = MAD_GAUSS_SEIDEL;
   d->precision = MAD_FP32;
   d->device = -1;
+  d->nranks = 1;
+  d->rank = 0;
   return MAD_OK;
 }
 
@@ -289,11 +335,13 @@ int mad_ved_create(const mad_ved_desc* d, mad_ved_ctx** out) {
     md.verbose = d->verbose;
     md.precision = d->precision;
     md.device = d->device;
+    md.nranks = d->nranks < 1 ? 1 : d->nranks;
+    md.rank = d->rank;
     const int mrc = mad_create(&md, &v->mad);
     if (mrc != MAD_OK) throw MadError(mrc, g_last_error);
     for (int q = 0; q < 3; ++q) v->n[q] = d->size[q];
     v->N = v->n[0] * v->n[1] * v->n[2];
-    REQUIRE(v->n[0] <= INT32_MAX && v->n[1] <= INT32_MAX && v->n[2] <= 65535, MAD_ERR_INVALID,
+    REQUIRE(v->n[0] <= INT32_MAX && v->n[1] <= 65535 && v->n[2] <= 65535, MAD_ERR_INVALID,
             "image too large for the VED grid mapping");
     HIP_CHECK(hipSetDevice(v->mad->device));
     HIP_CHECK(hipMalloc(&v->img, sizeof(double) * v->N));
@@ -318,6 +366,16 @@ int mad_ved_run_device(mad_ved_ctx* v, const void* in, int32_t in_dtype, void* o
                        int32_t out_dtype, mad_ved_stats* st) {
   if (!v || !in || !out) return MAD_ERR_INVALID;
   return ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, true, st); });
+}
+
+int mad_ved_comm_init(mad_ved_ctx* v, const void* uid128) {
+  if (!v || !uid128) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] { mad_call(v->mad, mad_comm_init(v->mad, uid128)); });
+}
+
+int mad_ved_comm_init_local(mad_ved_ctx* v, uint64_t group) {
+  if (!v) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] { mad_call(v->mad, mad_comm_init_local(v->mad, group)); });
 }
 
 int mad_ved_tensor(mad_ved_ctx* v, const void* image, int32_t dtype, double* tensor_soa,

@@ -11,8 +11,8 @@
 // mad_ved.hpp): z (image -> 3 derivative orders), y (-> the 6 (y, z) order pairs the
 // Hessian needs), then x, fused with the per-voxel eigen-analysis, vesselness and the
 // running maximum over scales, so the 6 Hessian components never reach HBM.
-// Storage / FIR arithmetic in T (fp32 or fp64, explicit fma); the eigen-analysis,
-// vesselness, response and vessel direction are fp64 (the reference's Precision).
+// Storage, FIR and eigen arithmetic in T (fp32 or fp64, explicit fma); response and
+// vessel direction are stored in fp64 (the reference's Precision).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,114 +30,165 @@ struct VesselParams {
   double alpha, beta, gamma;
 };
 
+// The three passes stage their input lines through LDS once (each input value is read
+// from HBM once per pass plus the tile halo) and run the taps out of LDS.  Taps live in
+// a small device array read with uniform (scalar) loads: [K0 | K1 | K2], each 2R+1.
+
 // z pass: o_q(i,j,k) = sum_t K_q(t) in(i, j, clamp(k + t)), q = 0, 1, 2 (orders).
-// taps: [K0 | K1 | K2], each 2R+1 long.  Reads of `in` (fp64 image) are coalesced in x.
+// Block = 64 x 4 columns, ZT output planes; LDS holds the ZT + 2R input planes of the
+// block's columns (converted from the fp64 image to T on the way in).
 template <typename T>
 __global__ void __launch_bounds__(256) ved_fir_z_k(const double* __restrict__ in, T* __restrict__ o0,
                                                    T* __restrict__ o1, T* __restrict__ o2,
                                                    const T* __restrict__ taps, int R, int nx, int ny,
-                                                   int nz) {
+                                                   int nz, int ZT) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = blockIdx.y * blockDim.y + threadIdx.y;
-  const int k = blockIdx.z;
-  if (i >= nx || j >= ny) return;
+  extern __shared__ __align__(16) unsigned char ved_smem[];
+  T* L = reinterpret_cast<T*>(ved_smem);
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x * 64 + (tid & 63);
+  const int j = blockIdx.y * 4 + (tid >> 6);
+  const int z0 = blockIdx.z * ZT;
+  const bool ok = i < nx && j < ny;
   const int64_t sz = (int64_t)nx * ny;
-  const int64_t col = (int64_t)j * nx + i;
-  const int W = 2 * R + 1;
-  T a0 = T(0), a1 = T(0), a2 = T(0);
-  for (int t = -R; t <= R; ++t) {
-    const int kk = min(max(k + t, 0), nz - 1);
-    const T v = (T)in[kk * sz + col];
-    a0 = fma(taps[t + R], v, a0);
-    a1 = fma(taps[W + t + R], v, a1);
-    a2 = fma(taps[2 * W + t + R], v, a2);
+  const int64_t col = (int64_t)min(j, ny - 1) * nx + min(i, nx - 1);
+  const int np = ZT + 2 * R;
+  for (int m = 0; m < np; ++m) {
+    const int kk = min(max(z0 - R + m, 0), nz - 1);
+    L[m * 256 + tid] = (T)in[kk * sz + col];
   }
-  const int64_t p = k * sz + col;
-  o0[p] = a0;
-  o1[p] = a1;
-  o2[p] = a2;
+  // each thread reads only its own column: no barrier needed
+  const int W = 2 * R + 1;
+  const int zend = min(ZT, nz - z0);
+  for (int o = 0; o < zend; ++o) {
+    T a0 = T(0), a1 = T(0), a2 = T(0);
+    const T* c = L + o * 256 + tid;
+#pragma unroll 4
+    for (int q = 0; q < W; ++q) {
+      const T v = c[q * 256];
+      a0 = fma(taps[q], v, a0);
+      a1 = fma(taps[W + q], v, a1);
+      a2 = fma(taps[2 * W + q], v, a2);
+    }
+    if (ok) {
+      const int64_t p = (int64_t)(z0 + o) * sz + col;
+      o0[p] = a0;
+      o1[p] = a1;
+      o2[p] = a2;
+    }
+  }
 }
 
 // y pass: the six (y order, z order) pairs of the Hessian:
 //   a00 = K0y z0, a10 = K1y z0, a20 = K2y z0, a01 = K0y z1, a11 = K1y z1, a02 = K0y z2
+// Block = 64 x-columns of one plane, YT output rows; LDS holds the YT + 2R input rows
+// of the three inputs; each thread produces YT / 4 outputs of its column.
 template <typename T>
 __global__ void __launch_bounds__(256) ved_fir_y_k(const T* __restrict__ z0, const T* __restrict__ z1,
                                                    const T* __restrict__ z2, T* __restrict__ a00,
                                                    T* __restrict__ a10, T* __restrict__ a20,
                                                    T* __restrict__ a01, T* __restrict__ a11,
                                                    T* __restrict__ a02, const T* __restrict__ taps,
-                                                   int R, int nx, int ny, int nz) {
+                                                   int R, int nx, int ny, int nz, int YT) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  extern __shared__ __align__(16) unsigned char ved_smem[];
+  T* L = reinterpret_cast<T*>(ved_smem);
+  const int tid = threadIdx.x;
+  const int xi = tid & 63;
+  const int i = blockIdx.x * 64 + xi;
+  const int y0 = blockIdx.y * YT;
   const int k = blockIdx.z;
-  if (i >= nx || j >= ny) return;
   const int64_t sz = (int64_t)nx * ny;
-  const int64_t pl = k * sz + i;
-  const int W = 2 * R + 1;
-  T s00 = T(0), s10 = T(0), s20 = T(0), s01 = T(0), s11 = T(0), s02 = T(0);
-  for (int t = -R; t <= R; ++t) {
-    const int jj = min(max(j + t, 0), ny - 1);
+  const int64_t pl = (int64_t)k * sz + min(i, nx - 1);
+  const int nr = YT + 2 * R;
+  const int64_t S3 = (int64_t)nr * 64;  // one input's slab in LDS
+  for (int r = tid >> 6; r < nr; r += 4) {
+    const int jj = min(max(y0 - R + r, 0), ny - 1);
     const int64_t q = pl + (int64_t)jj * nx;
-    const T v0 = z0[q], v1 = z1[q], v2 = z2[q];
-    const T k0 = taps[t + R], k1 = taps[W + t + R], k2 = taps[2 * W + t + R];
-    s00 = fma(k0, v0, s00);
-    s10 = fma(k1, v0, s10);
-    s20 = fma(k2, v0, s20);
-    s01 = fma(k0, v1, s01);
-    s11 = fma(k1, v1, s11);
-    s02 = fma(k0, v2, s02);
+    L[r * 64 + xi] = z0[q];
+    L[S3 + r * 64 + xi] = z1[q];
+    L[2 * S3 + r * 64 + xi] = z2[q];
   }
-  const int64_t p = pl + (int64_t)j * nx;
-  a00[p] = s00;
-  a10[p] = s10;
-  a20[p] = s20;
-  a01[p] = s01;
-  a11[p] = s11;
-  a02[p] = s02;
+  __syncthreads();
+  if (i >= nx) return;
+  const int W = 2 * R + 1;
+  const int yend = min(YT, ny - y0);
+  for (int o = tid >> 6; o < yend; o += 4) {
+    T s00 = T(0), s10 = T(0), s20 = T(0), s01 = T(0), s11 = T(0), s02 = T(0);
+    const T* c = L + o * 64 + xi;
+#pragma unroll 4
+    for (int q = 0; q < W; ++q) {
+      const T v0 = c[q * 64], v1 = c[S3 + q * 64], v2 = c[2 * S3 + q * 64];
+      const T k0 = taps[q], k1 = taps[W + q], k2 = taps[2 * W + q];
+      s00 = fma(k0, v0, s00);
+      s10 = fma(k1, v0, s10);
+      s20 = fma(k2, v0, s20);
+      s01 = fma(k0, v1, s01);
+      s11 = fma(k1, v1, s11);
+      s02 = fma(k0, v2, s02);
+    }
+    const int64_t p = pl + (int64_t)(y0 + o) * nx;
+    a00[p] = s00;
+    a10[p] = s10;
+    a20[p] = s20;
+    a01[p] = s01;
+    a11[p] = s11;
+    a02[p] = s02;
+  }
 }
 
-// Symmetric 3x3 eigen-decomposition by cyclic Jacobi rotations (fp64): w ascending,
-// V columns the matching unit eigenvectors -- the order vnl_symmetric_eigensystem
-// returns (VED.hxx:259-264).  Converges quadratically; stops when the off-diagonal
-// mass is below 1e-17 of the diagonal's.
-__device__ inline void sym3_eigen(double a00, double a01, double a02, double a11, double a12,
-                                  double a22, double w[3], double V[3][3]) {
+// Symmetric 3x3 eigen-decomposition by cyclic Jacobi rotations in E (fp64, or fp32
+// in the fp32 storage mode): w ascending, V columns the matching unit eigenvectors --
+// the order vnl_symmetric_eigensystem returns (VED.hxx:259-264).  Converges
+// quadratically; stops when the off-diagonal mass is below ~eps/16 of the diagonal's.
+template <typename E>
+struct EigLimits;
+template <>
+struct EigLimits<double> {
+  static constexpr double conv = 1e-17, tiny = 1e-300, huge = 1e150;
+};
+template <>
+struct EigLimits<float> {
+  static constexpr float conv = 1e-8f, tiny = 1e-30f, huge = 1e18f;
+};
+
+template <typename E>
+__device__ inline void sym3_eigen(E a00, E a01, E a02, E a11, E a12, E a22, E w[3], E V[3][3]) {
 #pragma clang fp contract(off)
-  double A[3][3] = {{a00, a01, a02}, {a01, a11, a12}, {a02, a12, a22}};
+  using Lim = EigLimits<E>;
+  E A[3][3] = {{a00, a01, a02}, {a01, a11, a12}, {a02, a12, a22}};
   for (int r = 0; r < 3; ++r)
-    for (int c = 0; c < 3; ++c) V[r][c] = (r == c) ? 1.0 : 0.0;
+    for (int c = 0; c < 3; ++c) V[r][c] = (r == c) ? E(1) : E(0);
   for (int sweep = 0; sweep < 24; ++sweep) {
-    const double off = fabs(A[0][1]) + fabs(A[0][2]) + fabs(A[1][2]);
-    const double dia = fabs(A[0][0]) + fabs(A[1][1]) + fabs(A[2][2]);
-    if (!(off > 1e-17 * dia) || off < 1e-300) break;
+    const E off = fabs(A[0][1]) + fabs(A[0][2]) + fabs(A[1][2]);
+    const E dia = fabs(A[0][0]) + fabs(A[1][1]) + fabs(A[2][2]);
+    if (!(off > Lim::conv * dia) || off < Lim::tiny) break;
 #pragma unroll
     for (int pq = 0; pq < 3; ++pq) {
       const int p = pq == 2 ? 1 : 0;
       const int q = pq == 0 ? 1 : 2;
       const int r = 3 - p - q;
-      const double apq = A[p][q];
-      if (fabs(apq) < 1e-300) continue;
-      const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-      double t;
-      if (fabs(theta) > 1e150) {
-        t = 0.5 / theta;
+      const E apq = A[p][q];
+      if (fabs(apq) < Lim::tiny) continue;
+      const E theta = (A[q][q] - A[p][p]) / (E(2) * apq);
+      E t;
+      if (fabs(theta) > Lim::huge) {
+        t = E(0.5) / theta;
       } else {
-        t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-        if (theta < 0.0) t = -t;
+        t = E(1) / (fabs(theta) + sqrt(theta * theta + E(1)));
+        if (theta < E(0)) t = -t;
       }
-      const double c = 1.0 / sqrt(t * t + 1.0);
-      const double s = t * c;
+      const E c = E(1) / sqrt(t * t + E(1));
+      const E s = t * c;
       A[p][p] -= t * apq;
       A[q][q] += t * apq;
-      A[p][q] = A[q][p] = 0.0;
-      const double arp = A[r][p], arq = A[r][q];
+      A[p][q] = A[q][p] = E(0);
+      const E arp = A[r][p], arq = A[r][q];
       A[r][p] = A[p][r] = c * arp - s * arq;
       A[r][q] = A[q][r] = s * arp + c * arq;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const double vkp = V[k][p], vkq = V[k][q];
+        const E vkp = V[k][p], vkq = V[k][q];
         V[k][p] = c * vkp - s * vkq;
         V[k][q] = s * vkp + c * vkq;
       }
@@ -149,12 +200,12 @@ __device__ inline void sym3_eigen(double a00, double a01, double a02, double a11
   // ascending, columns with them
   auto sw = [&](int a, int b) {
     if (w[a] > w[b]) {
-      const double tw = w[a];
+      const E tw = w[a];
       w[a] = w[b];
       w[b] = tw;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const double tv = V[k][a];
+        const E tv = V[k][a];
         V[k][a] = V[k][b];
         V[k][b] = tv;
       }
@@ -165,19 +216,20 @@ __device__ inline void sym3_eigen(double a00, double a01, double a02, double a11
   sw(0, 1);
 }
 
-// VesselnessFunction (VED.hxx:176-212) on eigenvalues sorted by magnitude; the
+// VesselnessFunction (VED.hxx:176-212) on eigenvalues sorted by magnitude, in E; the
 // reference's unqualified abs() on doubles is fabs.
-__device__ inline double ved_vesselness(double e0, double e1, double e2, const VesselParams& vp) {
-  if (e1 >= 0.0 || e2 >= 0.0) return 0.0;
-  const double smoothC = 1e-5;
-  const double aden = 2.0 * vp.alpha * vp.alpha;
-  const double bden = 2.0 * vp.beta * vp.beta;
-  const double gden = 2.0 * vp.gamma * vp.gamma;
-  const double anum = (e1 * e1) / (e2 * e2);
-  const double bnum = (e0 * e0) / fabs(e1 * e2);
-  const double gnum = (e0 * e0) + (e1 * e1) + (e2 * e2);
-  const double sf = exp(-(2 * smoothC * smoothC) / (fabs(e1) * e2 * e2));
-  return sf * (1. - exp(-anum / aden)) * exp(-bnum / bden) * (1. - exp(-gnum / gden));
+template <typename E>
+__device__ inline E ved_vesselness(E e0, E e1, E e2, const VesselParams& vp) {
+  if (e1 >= E(0) || e2 >= E(0)) return E(0);
+  const E smoothC = E(1e-5);
+  const E aden = E(2.0 * vp.alpha * vp.alpha);
+  const E bden = E(2.0 * vp.beta * vp.beta);
+  const E gden = E(2.0 * vp.gamma * vp.gamma);
+  const E anum = (e1 * e1) / (e2 * e2);
+  const E bnum = (e0 * e0) / fabs(e1 * e2);
+  const E gnum = (e0 * e0) + (e1 * e1) + (e2 * e2);
+  const E sf = exp(-(E(2) * smoothC * smoothC) / (fabs(e1) * e2 * e2));
+  return sf * (E(1) - exp(-anum / aden)) * exp(-bnum / bden) * (E(1) - exp(-gnum / gden));
 }
 
 enum { VED_HESSIAN = 0, VED_UPDATE = 1 };
@@ -196,23 +248,40 @@ __global__ void __launch_bounds__(256) ved_fir_x_k(const T* __restrict__ a00, co
                                                    double* __restrict__ resp, double* __restrict__ dir,
                                                    int first, VesselParams vp) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  // block = 256 consecutive x of one row; LDS: the six input rows over [x0-R, x0+256+R)
+  extern __shared__ __align__(16) unsigned char ved_smem[];
+  T* L = reinterpret_cast<T*>(ved_smem);
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * 256;
+  const int i = x0 + tid;
+  const int j = blockIdx.y;
   const int k = blockIdx.z;
-  if (i >= nx || j >= ny) return;
   const int64_t n = (int64_t)nx * ny * nz;
   const int64_t row = ((int64_t)k * ny + j) * nx;
+  const int nw = 256 + 2 * R;
+  for (int e = tid; e < nw; e += 256) {
+    const int64_t q = row + min(max(x0 - R + e, 0), nx - 1);
+    L[e] = a00[q];
+    L[nw + e] = a10[q];
+    L[2 * nw + e] = a20[q];
+    L[3 * nw + e] = a01[q];
+    L[4 * nw + e] = a11[q];
+    L[5 * nw + e] = a02[q];
+  }
+  __syncthreads();
+  if (i >= nx) return;
   const int W = 2 * R + 1;
   T hxx = T(0), hxy = T(0), hyy = T(0), hxz = T(0), hyz = T(0), hzz = T(0);
-  for (int t = -R; t <= R; ++t) {
-    const int64_t q = row + min(max(i + t, 0), nx - 1);
-    const T k0 = taps[t + R], k1 = taps[W + t + R], k2 = taps[2 * W + t + R];
-    hxx = fma(k2, a00[q], hxx);
-    hxy = fma(k1, a10[q], hxy);
-    hyy = fma(k0, a20[q], hyy);
-    hxz = fma(k1, a01[q], hxz);
-    hyz = fma(k0, a11[q], hyz);
-    hzz = fma(k0, a02[q], hzz);
+  const T* c = L + tid;
+#pragma unroll 4
+  for (int q = 0; q < W; ++q) {
+    const T k0 = taps[q], k1 = taps[W + q], k2 = taps[2 * W + q];
+    hxx = fma(k2, c[q], hxx);
+    hxy = fma(k1, c[nw + q], hxy);
+    hyy = fma(k0, c[2 * nw + q], hyy);
+    hxz = fma(k1, c[3 * nw + q], hxz);
+    hyz = fma(k0, c[4 * nw + q], hyz);
+    hzz = fma(k0, c[5 * nw + q], hzz);
   }
   const double H0 = (double)hxx * hs.f[0], H1 = (double)hxy * hs.f[1], H2 = (double)hxz * hs.f[2];
   const double H3 = (double)hyy * hs.f[3], H4 = (double)hyz * hs.f[4], H5 = (double)hzz * hs.f[5];
@@ -226,19 +295,21 @@ __global__ void __launch_bounds__(256) ved_fir_x_k(const T* __restrict__ a00, co
     hess[5 * n + p] = H5;
     return;
   }
-  double w[3], V[3][3];
-  sym3_eigen(H0, H1, H2, H3, H4, H5, w, V);
+  // eigen-analysis and vesselness in the storage precision T (fp64 = the reference's
+  // Precision; fp32 in the fp32 mode, like the solver)
+  T w[3], V[3][3];
+  sym3_eigen<T>((T)H0, (T)H1, (T)H2, (T)H3, (T)H4, (T)H5, w, V);
   // sort by magnitude with the reference's three swaps (VED.hxx:266-268)
-  double e0 = w[0], e1 = w[1], e2 = w[2], tt;
+  T e0 = w[0], e1 = w[1], e2 = w[2], tt;
   if (fabs(e0) > fabs(e1)) { tt = e0; e0 = e1; e1 = tt; }
   if (fabs(e1) > fabs(e2)) { tt = e1; e1 = e2; e2 = tt; }
   if (fabs(e0) > fabs(e1)) { tt = e0; e0 = e1; e1 = tt; }
-  const double v = ved_vesselness(e0, e1, e2, vp);
+  const double v = (double)ved_vesselness<T>(e0, e1, e2, vp);
   if (first || v > resp[p]) {
     resp[p] = v;
-    dir[p] = V[0][2];
-    dir[n + p] = V[1][2];
-    dir[2 * n + p] = V[2][2];
+    dir[p] = (double)V[0][2];
+    dir[n + p] = (double)V[1][2];
+    dir[2 * n + p] = (double)V[2][2];
   }
 }
 

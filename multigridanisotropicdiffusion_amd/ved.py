@@ -26,7 +26,7 @@ class VED:
                  scales=(0.300, 0.482, 0.775, 1.245, 2.000), iterations=1,
                  diffusion_iterations=5, cycle=C.VCYCLE, time_step=0.1, tolerance=1e-6,
                  diffusion_iterations_per_grid=2, verbose=False, smoother=C.GAUSS_SEIDEL,
-                 precision=C.FP32, device=-1):
+                 precision=C.FP32, device=-1, nranks=1, rank=0):
         if len(shape) != 3:
             raise ValueError("VED is 3D (itkVEDMultigridImageFilter.h:46)")
         if len(scales) > C.VED_MAX_SCALES:
@@ -49,7 +49,14 @@ class VED:
         d.diffusion_iterations_per_grid = diffusion_iterations_per_grid
         d.verbose = int(bool(verbose))
         d.smoother, d.precision, d.device = int(smoother), int(precision), int(device)
+        d.nranks, d.rank = int(nranks), int(rank)
         self.desc = d
+        self.nranks, self.rank = int(nranks), int(rank)
+        nz = self.shape[0]
+        if nz % self.nranks:
+            raise ValueError(f"nz {nz} not divisible by nranks {self.nranks}")
+        per = nz // self.nranks
+        self.slab = (per * self.rank, per * (self.rank + 1))  # this rank's output planes
         ctx = ctypes.c_void_p()
         rc = self._L.mad_ved_create(ctypes.byref(d), ctypes.byref(ctx))
         if rc != C.OK:
@@ -64,6 +71,14 @@ class VED:
     def __del__(self):
         self.close()
 
+    def comm_init(self, uid):
+        """Join the RCCL communicator (uid from solver.comm_unique_id() on rank 0)."""
+        self._check(self._L.mad_ved_comm_init(self._ctx, ctypes.c_char_p(bytes(uid))))
+
+    def comm_init_local(self, group):
+        """In-process transport: ranks as threads of this process on one device."""
+        self._check(self._L.mad_ved_comm_init_local(self._ctx, ctypes.c_uint64(group)))
+
     def _check(self, rc):
         if rc != C.OK:
             raise C.MadError(rc, (self._L.mad_ved_last_error(self._ctx) or b"").decode())
@@ -75,9 +90,10 @@ class VED:
         return img
 
     def run(self, image, out_dtype=np.float64):
-        """GenerateData on a host image; returns (output, stats dict)."""
+        """GenerateData on a host image (the whole volume on every rank); returns (this
+        rank's z-slab of the output -- the whole volume on one GPU --, stats dict)."""
         img = self._img(image)
-        out = np.empty(self.shape, dtype=out_dtype)
+        out = np.empty((self.slab[1] - self.slab[0],) + self.shape[1:], dtype=out_dtype)
         st = C.VedStats()
         self._check(self._L.mad_ved_run(self._ctx, img.ctypes.data_as(ctypes.c_void_p),
                                         mad_dtype(img.dtype), out.ctypes.data_as(ctypes.c_void_p),

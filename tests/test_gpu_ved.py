@@ -3,8 +3,10 @@
 
 Tolerances (written per test):
   Hessian: fp64 storage <= 1e-12 of max|H|; fp32 storage <= 2e-6 of max|H|.
-  Tensor / response (fp64 eigen-analysis on the fp64 Hessian): <= 1e-9 absolute
-    (Jacobi rotations vs LAPACK: rounding-level differences only).
+  Tensor / response, fp64 mode (fp64 Hessian and Jacobi eigen-analysis): response
+    <= 1e-9, tensor <= 1e-6 absolute (Jacobi rotations vs LAPACK: rounding level).
+  fp32 mode (fp32 Hessian and eigen-analysis): response <= 1e-4, tensor <= 1e-3
+    (V = resp^(1/10) amplifies the rounding of tiny responses).
   Whole filter on the reference's own test volume and parameters (itkVEDTest_GS.cxx):
     ||u_gpu - u_ref||_inf / ||u_ref||_inf <= 1e-5 (fp32, north-star bar), <= 1e-8 (fp64);
     short output: truncation of the same values, |diff| <= 1.
@@ -124,3 +126,40 @@ def test_constant_volume_is_a_fixed_point(M):
     T, resp = v.tensor(np.full(shape, 42.0))
     assert resp.max() == 0.0
     assert np.array_equal(T[0], np.ones(shape)) and np.array_equal(T[1], np.zeros(shape))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_ved_on_rank_slabs_matches_single(M, nranks):
+    """Multi-GPU VED rehearsed with the in-process transport (ranks as threads on one
+    device): replicated tensor generation, z-slab diffusion, slabs all-gathered between
+    the two VED iterations; the concatenated slabs equal the single-rank output."""
+    import threading
+    import zlib
+    shape = (64, 48, 40)
+    rng = np.random.default_rng(5)
+    img = (rng.normal(100.0, 20.0, size=shape)).astype(np.float32)
+    kw = dict(omega=1.5, iterations=2, diffusion_iterations=2, tolerance=1e-6,
+              scales=(0.5, 1.0, 2.0))
+    ref, rst = M.VED(shape, (1.0, 1.0, 1.0), **kw).run(img, out_dtype=np.float64)
+    outs, errs = [None] * nranks, []
+    key = zlib.crc32(repr(("ved", shape, nranks)).encode())
+
+    def worker(r):
+        try:
+            v = M.VED(shape, (1.0, 1.0, 1.0), nranks=nranks, rank=r, **kw)
+            v.comm_init_local(key)
+            outs[r] = v.run(img, out_dtype=np.float64)
+            v.close()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append((r, e))
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    full = np.concatenate([o[0] for o in outs])
+    assert full.shape == shape
+    assert np.abs(full - ref).max() <= 1e-5 * np.abs(ref).max()
+    assert all(o[1]["total_cycles"] == rst["total_cycles"] for o in outs)
