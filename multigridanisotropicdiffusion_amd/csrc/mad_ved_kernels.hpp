@@ -152,6 +152,16 @@ struct EigLimits<float> {
   static constexpr float conv = 1e-8f, tiny = 1e-30f, huge = 1e18f;
 };
 
+// rotation arithmetic: IEEE in fp64; the hardware reciprocal / square-root / reciprocal
+// square-root approximations (~1 ulp) in fp32, where the rotation only needs c^2 + s^2 = 1
+// to fp32 accuracy
+__device__ inline double ei_rcp(double x) { return 1.0 / x; }
+__device__ inline double ei_sqrt(double x) { return sqrt(x); }
+__device__ inline double ei_rsqrt(double x) { return 1.0 / sqrt(x); }
+__device__ inline float ei_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ inline float ei_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ inline float ei_rsqrt(float x) { return __builtin_amdgcn_rsqf(x); }
+
 template <typename E>
 __device__ inline void sym3_eigen(E a00, E a01, E a02, E a11, E a12, E a22, E w[3], E V[3][3]) {
 #pragma clang fp contract(off)
@@ -170,15 +180,15 @@ __device__ inline void sym3_eigen(E a00, E a01, E a02, E a11, E a12, E a22, E w[
       const int r = 3 - p - q;
       const E apq = A[p][q];
       if (fabs(apq) < Lim::tiny) continue;
-      const E theta = (A[q][q] - A[p][p]) / (E(2) * apq);
+      const E theta = (A[q][q] - A[p][p]) * ei_rcp(E(2) * apq);
       E t;
       if (fabs(theta) > Lim::huge) {
-        t = E(0.5) / theta;
+        t = E(0.5) * ei_rcp(theta);
       } else {
-        t = E(1) / (fabs(theta) + sqrt(theta * theta + E(1)));
+        t = ei_rcp(fabs(theta) + ei_sqrt(theta * theta + E(1)));
         if (theta < E(0)) t = -t;
       }
-      const E c = E(1) / sqrt(t * t + E(1));
+      const E c = ei_rsqrt(t * t + E(1));
       const E s = t * c;
       A[p][p] -= t * apq;
       A[q][q] += t * apq;
