@@ -5,6 +5,8 @@
 //     include/itkMultigridAnisotropicDiffusionImageFilter.h:89-160
 //   smoother plug-ins  mad::MultigridGaussSeidelSmoother<D> / MultigridWeightedJacobiSmoother<D>
 //     include/mad/itkMultigridGaussSeidelSmoother.h, itkMultigridWeightedJacobiSmoother.h
+//   itk::VEDMultigridImageFilter<TIn, TOut, TSmoother>
+//     include/itkVEDMultigridImageFilter.h:43-168 (through mad_ved.h)
 // ITK itself is not a dependency: images are the small mad::itkshim::Image below
 // (buffer + size + spacing + origin, x fastest, region index 0).  With a real
 // ITK build the same class body sits behind itk::ImageToImageFilter: GenerateData
@@ -21,6 +23,7 @@
 #include <vector>
 
 #include "mad.h"
+#include "mad_ved.h"
 
 namespace mad {
 namespace itkshim {
@@ -183,6 +186,85 @@ class MultigridAnisotropicDiffusionImageFilter {
   mad_stats stats_{};
   const TInputImage* input_ = nullptr;
   std::vector<double> tensor_;
+  typename TOutputImage::Pointer output_;
+};
+
+// itk::VEDMultigridImageFilter (VED.h:43-168): vessel enhancing diffusion, the caller of
+// the multigrid filter; the whole pipeline runs on the GPU through mad_ved.h.
+template <class TInputImage, class TOutputImage,
+          class TSmootherType = MultigridGaussSeidelSmoother<TInputImage::ImageDimension>>
+class VEDMultigridImageFilter {
+ public:
+  static_assert(TInputImage::ImageDimension == 3, "VED is 3D (VED.h:46)");
+  using Self = VEDMultigridImageFilter;
+  using Pointer = std::shared_ptr<Self>;
+  using InputPixelType = typename TInputImage::PixelType;
+  using OutputPixelType = typename TOutputImage::PixelType;
+  using Precision = double;
+  enum CycleType { VCYCLE = MAD_VCYCLE, FMG = MAD_FMG, SMOOTHER = MAD_SMOOTHER };
+
+  static Pointer New() { return Pointer(new Self()); }
+  ~VEDMultigridImageFilter() { mad_ved_destroy(ctx_); }
+
+  // setters (VED.h:88-106)
+  void SetAlpha(Precision v) { desc_.alpha = v; }
+  void SetBeta(Precision v) { desc_.beta = v; }
+  void SetGamma(Precision v) { desc_.gamma = v; }
+  void SetEpsilon(Precision v) { desc_.epsilon = v; }
+  void SetOmega(Precision v) { desc_.omega = v; }
+  void SetSensitivity(Precision v) { desc_.sensitivity = v; }
+  void SetScales(const std::vector<Precision>& s) {
+    if (s.empty() || s.size() > MAD_VED_MAX_SCALES) throw Error(MAD_ERR_INVALID, "1..16 scales");
+    desc_.nscales = (int32_t)s.size();
+    for (size_t q = 0; q < s.size(); ++q) desc_.scales[q] = s[q];
+  }
+  void SetIterations(unsigned int n) { desc_.iterations = n; }
+  void SetDiffusionIterations(unsigned int n) { desc_.diffusion_iterations = n; }
+  void SetCycle(CycleType c) { desc_.cycle = c; }
+  void SetTimeStep(Precision dt) { desc_.time_step = dt; }
+  void SetTolerance(Precision t) { desc_.tolerance = t; }
+  void SetDiffusionIterationsPerGrid(unsigned int n) { desc_.diffusion_iterations_per_grid = n; }
+  void SetVerbose(bool v) { desc_.verbose = v ? 1 : 0; }
+  // MI355X execution options (no reference counterpart)
+  void SetPrecision(int32_t p) { desc_.precision = p; }
+  void SetDevice(int32_t d) { desc_.device = d; }
+
+  void SetInput(const TInputImage* img) { input_ = img; }
+  typename TOutputImage::Pointer GetOutput() const { return output_; }
+  const mad_ved_stats& GetStats() const { return stats_; }
+
+  // GenerateData (VED.hxx:63-155)
+  void Update() {
+    if (!input_) throw Error(MAD_ERR_STATE, "SetInput first");
+    mad_ved_desc d = desc_;
+    for (unsigned q = 0; q < 3; ++q) {
+      d.size[q] = input_->GetSize()[q];
+      d.spacing[q] = input_->GetSpacing()[q];
+    }
+    d.smoother = TSmootherType::id;
+    mad_ved_destroy(ctx_);
+    ctx_ = nullptr;
+    if (int rc = mad_ved_create(&d, &ctx_))
+      throw Error(rc, std::string("mad_ved: ") + mad_ved_last_error(nullptr));
+    output_ = TOutputImage::New();
+    output_->SetRegions(input_->GetSize());
+    output_->Allocate();
+    output_->SetSpacing(input_->GetSpacing());
+    output_->SetOrigin(input_->GetOrigin());
+    if (int rc = mad_ved_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
+                             output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id,
+                             &stats_))
+      throw Error(rc, std::string("mad_ved: ") + mad_ved_last_error(ctx_));
+  }
+
+ protected:
+  VEDMultigridImageFilter() { check(mad_ved_desc_init(&desc_)); }
+
+ private:
+  mad_ved_desc desc_{};
+  mad_ved_ctx* ctx_ = nullptr;
+  mad_ved_stats stats_{};
+  const TInputImage* input_ = nullptr;
   typename TOutputImage::Pointer output_;
 };
 

@@ -2,6 +2,8 @@
 // test/itk2DDiffusionTest_WJ.cxx:47-109 uses the reference filter.
 //   facade_test host   -> host-only calls (no GPU): defaults + depth rule
 //   facade_test run    -> 2D filter run on the GPU, prints the output checksum
+//   facade_test ved    -> VEDMultigridImageFilter on a short 3D volume with a bright tube,
+//                         set up like test/itkVEDTest_GS.cxx:46-95
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -12,7 +14,47 @@ using ImageType = mad::itkshim::Image<float, 2>;
 using FilterType = mad::MultigridAnisotropicDiffusionImageFilter<
     ImageType, ImageType, mad::MultigridWeightedJacobiSmoother<2>>;
 
+using VolumeType = mad::itkshim::Image<short, 3>;
+using VedType = mad::VEDMultigridImageFilter<VolumeType, VolumeType, mad::MultigridGaussSeidelSmoother<3>>;
+
+static int run_ved() {
+  auto input = VolumeType::New();
+  input->SetRegions({40, 36, 32});
+  input->Allocate();
+  input->SetSpacing({0.3125, 0.3125, 0.5});
+  short* p = input->GetBufferPointer();
+  for (int z = 0; z < 32; ++z)
+    for (int y = 0; y < 36; ++y)
+      for (int x = 0; x < 40; ++x) {
+        const double d2 = (x - 20.0) * (x - 20.0) + (y - 18.0) * (y - 18.0);
+        p[(z * 36 + y) * 40 + x] = (short)(200.0 * std::exp(-d2 / 18.0) + ((x * 7 + y * 3 + z) % 11));
+      }
+  auto filter = VedType::New();
+  filter->SetCycle(VedType::VCYCLE);
+  filter->SetDiffusionIterationsPerGrid(3);
+  filter->SetInput(input.get());
+  filter->SetScales({0.300, 0.482, 0.775, 1.245, 2.000});
+  filter->SetAlpha(0.5);
+  filter->SetBeta(0.5);
+  filter->SetGamma(5.);
+  filter->SetEpsilon(0.01);
+  filter->SetSensitivity(10.);
+  filter->SetIterations(1);
+  filter->SetTolerance(1e-10);
+  filter->SetTimeStep(0.1);
+  filter->SetDiffusionIterations(4);
+  filter->SetOmega(1.5);
+  filter->Update();
+  auto out = filter->GetOutput();
+  long sum = 0;
+  for (int64_t i = 0; i < out->NumberOfPixels(); ++i) sum += out->GetBufferPointer()[i];
+  std::printf("ved ok cycles=%u relres=%.3e checksum=%ld\n", filter->GetStats().total_cycles,
+              filter->GetStats().last_relres, sum);
+  return filter->GetStats().iterations == 1 && filter->GetStats().total_cycles >= 4 ? 0 : 5;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "ved") == 0) return run_ved();
   const bool run = argc > 1 && std::strcmp(argv[1], "run") == 0;
   mad_desc d;
   mad_desc_init(&d);

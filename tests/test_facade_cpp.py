@@ -31,3 +31,10 @@ def test_facade_runs_filter(exe):
     r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "run ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_facade_runs_ved_filter(exe):
+    r = subprocess.run([exe, "ved"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ved ok" in r.stdout
