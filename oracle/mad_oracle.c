@@ -482,6 +482,35 @@ void ora_gs_color(const ora_ctx *c, int level, int ncolors, const double *in, co
   }
 }
 
+/* The same multicolour sweep on all host cores (OpenMP over the planes of one colour;
+ * the colouring makes the updates of one colour independent, so the result does not
+ * depend on the thread count).  CPU baseline only (bench.py cpu_baseline.parallel). */
+void ora_gs_color_omp(const ora_ctx *c, int level, int ncolors, const double *in,
+                      const double *b, double *out, int nthreads) {
+  const ora_level *L = &c->lev[level];
+  const int ic = nbidx(0, 0, 0);
+  if (out != in) memcpy(out, in, sizeof(double) * L->N);
+  for (int col = 0; col < ncolors; ++col) {
+#pragma omp parallel for num_threads(nthreads) schedule(static) collapse(2)
+    for (long z = 0; z < L->n[2]; ++z)
+      for (long y = 0; y < L->n[1]; ++y)
+        for (long x = (color_of(c->dim, ncolors, 0, y, z) == col) ? 0 : 1; x < L->n[0]; x += 2) {
+          if (color_of(c->dim, ncolors, x, y, z) != col) break;  /* row holds no point of col */
+          long p = x + L->n[0] * (y + L->n[1] * z);
+          const double *S = L->A + 27 * p;
+          double value = b[p];
+          for (int k = 0; k < c->noff; ++k) {
+            const int *o = c->off[k];
+            if (o[0] == 0 && o[1] == 0 && o[2] == 0) continue;
+            if (!inside3(L, x + o[0], y + o[1], z + o[2])) continue;
+            long q = (x + o[0]) + L->n[0] * ((y + o[1]) + L->n[1] * (z + o[2]));
+            value -= S[nbidx(o[0], o[1], o[2])] * out[q];
+          }
+          out[p] = value / S[ic];
+        }
+  }
+}
+
 /* WJ SingleIteration, WJ:33-102 */
 void ora_wj(const ora_ctx *c, int level, double omega, const double *in, const double *b,
             double *out) {

@@ -57,6 +57,9 @@ const double *ora_stencil(const ora_ctx *c, int level);
 void ora_gs_lex(const ora_ctx *c, int level, const double *x, const double *b, double *out);
 void ora_gs_color(const ora_ctx *c, int level, int ncolors, const double *x, const double *b,
                   double *out);
+/* ora_gs_color on nthreads host threads (OpenMP; identical result) -- CPU baseline only */
+void ora_gs_color_omp(const ora_ctx *c, int level, int ncolors, const double *x, const double *b,
+                      double *out, int nthreads);
 void ora_wj(const ora_ctx *c, int level, double omega, const double *x, const double *b,
             double *out);
 void ora_residual(const ora_ctx *c, int level, const double *x, const double *b, double *r);

@@ -66,6 +66,8 @@ def lib():
         for name in ("ora_gs_lex", "ora_residual"):
             getattr(L, name).argtypes = [ctypes.c_void_p, ctypes.c_int, dp, dp, dp]
         L.ora_gs_color.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp, dp]
+        L.ora_gs_color_omp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp, dp,
+                                       ctypes.c_int]
         L.ora_wj.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, dp, dp, dp]
         L.ora_restrict.argtypes = [ctypes.c_void_p, ctypes.c_int, dp, dp]
         L.ora_interpolate.argtypes = [ctypes.c_void_p, ctypes.c_int, dp, dp]
@@ -164,6 +166,12 @@ class Oracle:
     def gs_color(self, l, x, b, ncolors=4):
         out = self._out(l)
         lib().ora_gs_color(self._c, l, ncolors, _dp(self._in(x)), _dp(self._in(b)), _dp(out))
+        return out
+
+    def gs_color_omp(self, l, x, b, ncolors=4, nthreads=1):
+        out = self._out(l)
+        lib().ora_gs_color_omp(self._c, l, ncolors, _dp(self._in(x)), _dp(self._in(b)), _dp(out),
+                               int(nthreads))
         return out
 
     def wj(self, l, x, b, omega=2.0 / 3.0):

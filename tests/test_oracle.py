@@ -189,3 +189,15 @@ def test_c1_lena_converges(O):
     for k in ("wj_v", "wj_fmg", "gs_fmg"):
         assert np.abs(g[k] - ref).max() < 1e-3  # float32-stored outputs of 0..255 images
     assert int(g["gs_v_cycles"][0]) < int(g["wj_v_cycles"][0])
+
+
+@pytest.mark.parametrize("nthreads", [1, 3])
+def test_openmp_colour_sweep_equals_serial(oracle_mod, nthreads):
+    """ora_gs_color_omp (bench.py's parallel CPU baseline) is the serial multicolour sweep."""
+    import synth
+    for shape, T, nc in [((14, 16, 18), synth.random_spd((14, 16, 18), seed=2), 4),
+                         ((14, 16, 18), synth.random_spd((14, 16, 18), seed=2, offdiag=False), 2),
+                         ((18, 20), synth.random_spd((18, 20), seed=2), 4)]:
+        o = oracle_mod.Oracle(shape, (1.0,) * len(shape), T, 0.3)
+        b = synth.image(shape, seed=3)
+        np.testing.assert_array_equal(o.gs_color(0, b, b, nc), o.gs_color_omp(0, b, b, nc, nthreads))
