@@ -157,3 +157,30 @@ def test_kernel_entry_points_reject_null_context():
     assert L.mad_smooth(None, 0, 1) == C.ERR_INVALID
     assert L.mad_vcycle(None) == C.ERR_INVALID
     assert L.mad_num_levels(None) == -1
+
+
+def test_ved_desc_defaults_match_reference():
+    """itkVEDMultigridImageFilter.hxx:34-58 defaults (mad_ved_desc_init)."""
+    L = C.load()
+    d = C.VedDesc()
+    assert L.mad_ved_desc_init(ctypes.byref(d)) == C.OK
+    assert (d.alpha, d.beta, d.gamma, d.epsilon, d.omega, d.sensitivity) == (0.5, 0.5, 5.0, 0.01, 5.0, 10.0)
+    assert d.nscales == 5 and list(d.scales[:5]) == [0.300, 0.482, 0.775, 1.245, 2.000]
+    assert (d.iterations, d.diffusion_iterations, d.diffusion_iterations_per_grid) == (1, 5, 2)
+    assert d.cycle == C.VCYCLE and d.time_step == 0.1 and d.tolerance == 1e-6
+    assert d.nranks == 1 and d.rank == 0
+
+
+@pytest.mark.parametrize("field,value", [("nscales", 0), ("nscales", 17), ("sensitivity", 0.0),
+                                         ("abi_version", 99)])
+def test_ved_create_rejects_bad_descriptors(field, value):
+    """Validated before any device work (runs without a GPU)."""
+    L = C.load()
+    d = C.VedDesc()
+    L.mad_ved_desc_init(ctypes.byref(d))
+    d.size[0] = d.size[1] = d.size[2] = 16
+    setattr(d, field, value)
+    ctx = ctypes.c_void_p()
+    assert L.mad_ved_create(ctypes.byref(d), ctypes.byref(ctx)) == C.ERR_INVALID
+    assert not ctx.value
+    assert L.mad_ved_last_error(None)
