@@ -100,7 +100,9 @@ typedef struct mad_desc {
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
   int32_t rank;                  /* this rank */
   int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep, v3),
-                                    1 one launch per colour, 2 fused v2, 3 fused v3 */
+                                    1 one launch per colour, 2 fused v2, 3 fused v3,
+                                    4 fused v3 with the last z-chunk marched downward (the
+                                    rank-slab form, selectable on one GPU for parity) */
   int32_t reserved[8];
 } mad_desc;
 

@@ -577,11 +577,22 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
 // Needs: coefficient fields with >= 1 padding plane below and above every field
 // (LevelData::cf, GHOST planes) and x/b arrays with their GHOST planes; nx, ny >= 3.
 // LDS: dynamic, NP * PLANE * sizeof(T) bytes.
+//
+// Rank slabs (flip_last, sig): the LAST z-chunk of the launch marches downward -- the
+// kernel runs it on a z-reflected view of the slab (negative plane stride, ghost
+// sides swapped, +z / -z neighbour planes swapped back at the stencil, colour parity
+// from the physical plane), which gives bit-identical results because a multicolour
+// sweep does not depend on the order within a colour.  So the slab's first and last
+// GHOST planes are both final a few steps into the launch; the workgroups of the two
+// edge chunks then count themselves in sig[0] (bottom) / sig[1] (top), and the
+// communication stream, waiting on those counters, exchanges the halo while the rest
+// of the sweep runs -- one launch per sweep instead of boundary + interior launches.
 template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
-                                                        int zbase, int zstride) {
+                                                        int zbase, int zstride, int flip_last,
+                                                        uint32_t* __restrict__ sig) {
   constexpr int NC = (KIND == KFULL) ? 4 : 2;
   using FG = FusedGeom<NC, TX, TY>;
   constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
@@ -610,20 +621,40 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   const int tid = threadIdx.x;
   const int nx = g.nx, ny = g.ny;
   const int sy = (int)g.sy, hx0 = g.hx0;
-  const int64_t sz = g.sz;
   // tile whose region keeps >= 2 points from every x/y face: no masks, no ghost images
   const bool interior = rx0 >= 2 && rx0 + RX <= nx - 2 && ry0 >= 2 && ry0 + RY <= ny - 2;
 
-  const int zlo = g.zlo_ghost ? -GHOST : 0;
-  const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;
-  const int ulo = g.zlo_ghost ? -(GHOST - 1) : 0;
-  const int uhi = g.zhi_ghost ? g.nz + GHOST - 1 : g.nz;
   // chunk q of this launch covers owned planes [zbase + q*zstride, +zc): one launch
   // may cover a slab's two boundary chunks only, or its interior (rank-slab overlap)
-  const int z0 = zbase + chunk * zstride;
-  const int z1 = min(z0 + zc, g.nz);
+  const int p0 = zbase + chunk * zstride;
+  const int p1 = min(p0 + zc, g.nz);
+  // z-reflected view for a downward-marching last chunk: logical plane l = physical
+  // nz-1-l (all plane addressing below goes through sz, zlo_g / zhi_g, zpar)
+  const bool flip = flip_last != 0 && chunk == (int)(gridDim.x / tiles) - 1;
+  int64_t sz = g.sz;
+  int zlo_g = g.zlo_ghost, zhi_g = g.zhi_ghost, zpar = g.zoff;
+  int z0 = p0, z1 = p1;
+  if (flip) {
+    const int64_t top = (int64_t)(g.nz - 1) * g.sz;
+    uin += top;
+    uout += top;
+    b += top;
+    cf += top * RS;
+    sz = -g.sz;
+    zlo_g = g.zhi_ghost;
+    zhi_g = g.zlo_ghost;
+    zpar = g.zoff + g.nz - 1;  // global parity of logical l = (l + zpar) & 1
+    z0 = g.nz - p1;
+    z1 = g.nz - p0;
+  }
+  const int zlo = zlo_g ? -GHOST : 0;
+  const int zhi = zhi_g ? g.nz + GHOST : g.nz;
+  const int ulo = zlo_g ? -(GHOST - 1) : 0;
+  const int uhi = zhi_g ? g.nz + GHOST - 1 : g.nz;
+  // an edge chunk of a rank slab signals once its first GHOST planes are final
+  const bool signals = sig != nullptr && z0 == 0 && zlo_g;
   // first step with its plane parity normalised to even (global z), last step
-  const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + g.zoff) & 1);
+  const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + zpar) & 1);
   const int kend = z1 + NC - 2;
 
   auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
@@ -759,12 +790,13 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   auto stage = [&](int c, int k, int PM) {
     const int m = k - c;
     if (!stage_on(c, m)) return;
-    const int zm = (m == 0 && !g.zlo_ghost) ? 1 : m - 1;
-    const int zp = (m == g.nz - 1 && !g.zhi_ghost) ? g.nz - 2 : m + 1;
+    const int zm = (m == 0 && !zlo_g) ? 1 : m - 1;
+    const int zp = (m == g.nz - 1 && !zhi_g) ? g.nz - 2 : m + 1;
     const uint32_t o = pl[c][PM % NPM] + (uint32_t)(pdelta(c, PM).l * (int)TS);
     unsigned char* A0 = lbytes + slot(m) * (PLANE * TS) + o;
-    const unsigned char* Am = lbytes + slot(zm) * (PLANE * TS) + o;
-    const unsigned char* Ap = lbytes + slot(zp) * (PLANE * TS) + o;
+    // physical -z / +z neighbour planes (swapped in the reflected view)
+    const unsigned char* Am = lbytes + slot(flip ? zp : zm) * (PLANE * TS) + o;
+    const unsigned char* Ap = lbytes + slot(flip ? zm : zp) * (PLANE * TS) + o;
     // li parity: NC=4 compile-time ((c+1+(1^PM)) & 1); NC=2 per thread (row parity)
     bool odd;
     if (NC == 4) {
@@ -872,6 +904,13 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
             if (q < TX * TY && gi < nx && gj < ny)
               buf_store<T, MAD_ST_AUX>(*reinterpret_cast<const T*>(P + (lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS),
                            ro, (uint32_t)(gj * sy + gi) * TS);
+          }
+          if (signals && mo == GHOST - 1) {
+            // the edge planes 0..GHOST-1 of this tile are stored: release them, count in
+            __threadfence();
+            __syncthreads();
+            if (tid == 0)
+              __hip_atomic_fetch_add(sig + (flip ? 1 : 0), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
       }

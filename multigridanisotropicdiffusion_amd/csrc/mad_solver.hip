@@ -270,6 +270,10 @@ struct LevelData {
   bool x_halo_pending = false;
   hipEvent_t ev_bnd = nullptr;   // boundary chunks of the fused sweep done
   hipEvent_t ev_halo = nullptr;  // their exchange done (communication stream)
+  // single-launch rank-slab sweeps: edge-plane counters the sweep kernel increments
+  // (signal memory, [0] bottom / [1] top) and the sweeps issued so far
+  uint32_t* sig = nullptr;
+  uint32_t sig_epoch = 0;
 };
 constexpr int kBoundaryPlanes = 8;  // z-depth of a rank slab's boundary chunks (>= GHOST)
 
@@ -334,10 +338,27 @@ class Solver final : public SolverBase {
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
+    int can_wait = 0;
+    if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, c->device) !=
+        hipSuccess)
+      can_wait = 0;
     for (int l = 0; l < nl; ++l)
       if (c->geom[l].distributed) {
         HIP_CHECK(hipEventCreateWithFlags(&lv_[l].ev_bnd, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&lv_[l].ev_halo, hipEventDisableTiming));
+        // single-launch rank-slab sweeps (part 3) with gs_kernel 4 only.  Not the
+        // default: the communication stream's wait-on-value wakes ~0.25 ms after the
+        // signal (tools/overlap_probe.hip, profiles/r01_overlap_probe.log) -- longer
+        // than a whole 64-plane rank sweep -- while an event after the short boundary
+        // launch releases the exchange within ~0.05 ms, so boundary + interior
+        // launches (parts 1, 2) win.
+        if (can_wait && c->d.gs_kernel == 4) {
+          HIP_CHECK(hipExtMallocWithFlags((void**)&lv_[l].sig, 2 * sizeof(uint32_t),
+                                          hipMallocSignalMemory));
+          const uint32_t zero[2] = {0u, 0u};
+          HIP_CHECK(hipMemcpy(lv_[l].sig, zero, sizeof zero, hipMemcpyHostToDevice));
+          lv_[l].sig_epoch = 0;
+        }
       }
     part_need = std::max<int64_t>(part_need, 4096);
     HIP_CHECK(hipMalloc(&part_, sizeof(double) * part_need));
@@ -447,10 +468,10 @@ class Solver final : public SolverBase {
   static int64_t margin_elems(const Geo& g) { return 48 * g.sy + 512; }
 
   bool use_fused(int l) const {
-    const int v = c_->d.gs_kernel;  // 0 auto (v3), 1 per-colour passes, 2 fused v2, 3 fused v3
+    const int v = c_->d.gs_kernel;  // 0 auto (v3), 1 per-colour passes, 2 fused v2, 3 / 4 fused v3
     if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL) return false;
     if (v == 1) return false;
-    if (v == 2 || v == 3) return true;
+    if (v >= 2) return true;
     // auto: the fused sweep marches each tile column through z sequentially, so it
     // needs a large slab to fill the chip; below ~4M voxels one launch per colour is
     // faster (measured: 256^3 fused 0.23 ms vs 0.28 ms, 128^3 fused 0.13 vs 0.064 ms)
@@ -495,13 +516,24 @@ class Solver final : public SolverBase {
     return ZRange{0, zc, zc, (nz + zc - 1) / zc};
   }
 
+  // parts: 0 whole slab, 1 the two boundary chunks, 2 the interior between them,
+  // 3 whole slab with the last chunk marched downward and the edge-plane signals
+  // (single-launch rank-slab sweep); gs_kernel 4 runs part 0 with the downward last
+  // chunk (no signals)
   template <int KD, int TX, int TY, int NT>
   void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
     const int nz = L.g.nz;
     ZRange zr = whole_range(nz, tiles, fc);
-    if (part == 1) {  // the two boundary chunks of a rank slab (they produce the halo planes)
+    int flip = (c_->d.gs_kernel == 4 && part == 0) ? 1 : 0;
+    uint32_t* sig = nullptr;
+    if (part == 3) {
+      zr = whole_range(nz, tiles, fc);
+      REQUIRE(zr.nchunks >= 2 && zr.zc >= GHOST, MAD_ERR_UNSUPPORTED, "slab too thin for the single-launch sweep");
+      flip = 1;
+      sig = L.sig;
+    } else if (part == 1) {  // the two boundary chunks of a rank slab (they produce the halo planes)
       zr = ZRange{0, kBoundaryPlanes, nz - kBoundaryPlanes, 2};
     } else if (part == 2) {  // the interior between them
       const int ni = nz - 2 * kBoundaryPlanes;
@@ -534,7 +566,7 @@ class Solver final : public SolverBase {
         attr = true;
       }
       hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zr.zc, ntx, nty, zr.zbase, zr.zstride);
+                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig);
     };
     if (L.brec)
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
@@ -542,6 +574,20 @@ class Solver final : public SolverBase {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>);
     else
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+  }
+
+
+  // tiles per plane and z-chunks of a whole-slab fused launch at level L
+  void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {
+    const FusedCfg& fc = fused_cfg();
+    int tx = 64, ty = 16;
+    if (c_->kind == KFULL) {
+      if (fc.tile == 1) ty = 32;
+      if (fc.tile == 2) tx = 128;
+      if (fc.tile == 3) { tx = 128; ty = 8; }
+    }
+    *tiles = ((L.g.nx + tx - 1) / tx) * ((L.g.ny + ty - 1) / ty);
+    *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
   }
 
   void launch_fused_part(LevelData<T>& L, int part) {
@@ -590,6 +636,16 @@ class Solver final : public SolverBase {
       const int lead = (!brec && kind == KFULL && fc.lead == 3) ? 3 : 2;
       std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d%s>", tn, kind, tx, ty,
                     nt, sizeof(T) == 8 ? 2 : 4, lead, brec ? ", true" : "");
+      // rank slabs: which sweep form fused_sweep takes
+      const LevelData<T>& L = lv_[l];
+      if (c_->comm.active() && c_->geom[l].distributed && c_->d.gs_kernel != 2 &&
+          L.g.nz >= 3 * kBoundaryPlanes) {
+        int tiles = 0, nchunks = 0;
+        fused_shape(L, &tiles, &nchunks);
+        const bool single = L.sig && nchunks >= 2;
+        return std::string(buf) + (single ? " [rank slab: single launch, edge signals]"
+                                          : " [rank slab: boundary + interior launches]");
+      }
     }
     return buf;
   }
@@ -620,7 +676,9 @@ class Solver final : public SolverBase {
   // the neighbours need) run first, the exchange of their output then runs on the
   // communication stream while the interior chunks sweep, and the next consumer of
   // x's ghost planes waits for it (halo()).  Slabs thinner than 3 boundary chunks
-  // sweep in one launch and exchange afterwards.
+  // sweep in one launch and exchange afterwards.  gs_kernel 4 makes the boundary and
+  // interior launches one launch instead (part 3: edge chunks signal their finished
+  // edge planes to the communication stream, which waits on the counters).
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
@@ -633,7 +691,24 @@ class Solver final : public SolverBase {
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
     const bool dist = c_->comm.active() && c_->geom[l].distributed;
     const bool overlap = dist && c_->d.gs_kernel != 2 && L.g.nz >= 3 * kBoundaryPlanes;
-    if (!overlap) {
+    int tiles = 0, nchunks = 0;
+    if (overlap) fused_shape(L, &tiles, &nchunks);
+    if (overlap && L.sig && nchunks >= 2) {
+      // one launch: its two edge chunks march outward-in (the top one downward) and
+      // count their finished edge planes; the communication stream waits on those
+      // counters and exchanges while the rest of the sweep runs
+      launch_fused_part(L, 3);
+      wait_all_pending();  // (none expected: halo() above already waited)
+      const uint32_t target = ++L.sig_epoch * (uint32_t)tiles;
+      if (L.g.zlo_ghost)
+        HIP_CHECK(hipStreamWaitValue32(c_->comm_stream, L.sig, target, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      if (L.g.zhi_ghost)
+        HIP_CHECK(hipStreamWaitValue32(c_->comm_stream, L.sig + 1, target, hipStreamWaitValueGte,
+                                       0xFFFFFFFFu));
+      c_->comm.exchange_planes(L.t, L.g.sz, L.g.nz, GHOST, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
+                               std::is_same<T, double>::value, c_->comm_stream);
+      HIP_CHECK(hipEventRecord(L.ev_halo, c_->comm_stream));
+    } else if (!overlap) {
       // MAD_SPLIT_PROXY=1 (measurement only): launch a single-GPU slab as a rank slab's
       // boundary + interior parts, without the exchange (tools/bench_slab.py)
       static const bool proxy = std::getenv("MAD_SPLIT_PROXY") != nullptr;
@@ -1218,6 +1293,7 @@ class Solver final : public SolverBase {
     for (auto& L : lv_) {
       if (L.ev_bnd) (void)hipEventDestroy(L.ev_bnd);
       if (L.ev_halo) (void)hipEventDestroy(L.ev_halo);
+      if (L.sig) (void)hipFree(L.sig);
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);

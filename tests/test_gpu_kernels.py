@@ -181,14 +181,15 @@ def test_fused_gs_sweep_is_bitwise_per_colour_passes(shape, tensor, prec):
     """The single-launch fused sweeps (gs_fused_k v2 and gs_fused3_k v3: z-wavefront,
     overlapped tiles, z-chunks; v3 with mirror ghosts in LDS) equal NC in-place
     colour passes bit for bit, including partial tiles, partial z-chunks, odd sizes
-    and 3-point axes (both mirror images of one point)."""
+    and 3-point axes (both mirror images of one point); so does v3 with its last
+    z-chunk run on the z-reflected view (the rank-slab single-launch form)."""
     import multigridanisotropicdiffusion_amd as M
     import synth
     T = {"full": lambda: synth.random_spd(shape, seed=1),
          "diag": lambda: synth.random_spd(shape, seed=1, offdiag=False),
          "iso": lambda: synth.isotropic(shape)}[tensor]()
     outs = []
-    for variant in (1, 2, 3):
+    for variant in (1, 2, 3, 4):  # 4: v3 with the last z-chunk marched downward
         s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec, gs_kernel=variant)
         s.set_tensor(T)
         s.setup()
