@@ -185,6 +185,9 @@ def main():
             "algorithmic_bytes_per_launch": BYTES_PER_VOXEL_SMOOTH * units_per_launch}
     if traffic:
         roof["traffic_source"] = traffic.get("source")
+        # the same launch priced on its measured HBM bytes (PMC) instead of the algorithmic ones
+        roof["traffic_GBs"] = round(traffic["bytes_per_launch"] / (kern_ms * 1e-3) / 1e9, 1)
+        roof["traffic_frac"] = round(roof["traffic_GBs"] / PEAK_HBM_GBS, 4)
     line = {
         "metric": "Mvoxel-smooths/s (and V-cycles/s) at 512^3 fp32; achieved HBM GB/s vs peak",
         "value": round(value, 1),
