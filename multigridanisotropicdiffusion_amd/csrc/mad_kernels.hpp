@@ -1327,10 +1327,12 @@ __global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fin
   }
 }
 
-// interp3_k: fine tile TX x TY (one thread per fine point), fine planes [k0, k1);
-// coarse planes staged in a 4-slot LDS ring one fine plane ahead; the fine value of
-// the next plane is prefetched into a register.
-template <typename T, int ADD, int TX, int TY>
+// interp3_k: fine tile TX x TY (one thread per fine point), fine planes [k0, k1),
+// marched in groups of G planes: the coarse planes a group's taps span go into an
+// 8-slot LDS ring (only the ones not already there), and the fine values of the NEXT
+// group are loaded while this group is computed, so each thread keeps G loads in
+// flight (one plane at a time left the level-0 launch latency-bound at ~2.5 TB/s).
+template <typename T, int ADD, int TX, int TY, int G = 8>
 __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coarse, Geo gc,
                                                      T* __restrict__ fine, Geo gf, int cx, int cy,
                                                      int cz, int ncz, int kc, int ntx, int kbase,
@@ -1338,7 +1340,10 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
 #pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   constexpr int NT = TX * TY;
   constexpr int CXW = TX / 2 + 2, CYW = TY / 2 + 2, CP = CXW * CYW;
-  __shared__ T ring[4 * CP];
+  constexpr int NS = 8;           // ring slots
+  constexpr int SPAN = G / 2 + 2;  // most coarse planes one group of G fine planes taps
+  static_assert(SPAN <= NS && CP <= NT, "interp3_k ring geometry");
+  __shared__ T ring[NS * CP];
   const int tiles = ntx * ((gf.ny + TY - 1) / TY);
   const int chunk = blockIdx.x / tiles;
   const int t = blockIdx.x - chunk * tiles;
@@ -1360,39 +1365,58 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
   const int k0 = kbase + chunk * kc, k1 = min(k0 + kc, kend);
   const int64_t pxy = (int64_t)j * gf.sy + i;
   int last = INT_MIN;  // largest coarse plane (global) in the ring
-  T xn = (ADD && ok && k0 < k1) ? fine[pxy + gf.sz * (int64_t)k0] : T(0);
-  for (int k = k0; k < k1; ++k) {
-    int iz[2], jz[2];
-    T wz[2], vz2[2];
+  T xc[G], xn[G];
+  auto load_fine = [&](int kk, T* dst) {
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      dst[q] = (ADD && ok && kk + q < k1) ? fine[pxy + gf.sz * (int64_t)(kk + q)] : T(0);
+  };
+  load_fine(k0, xc);
+  for (int k = k0; k < k1; k += G) {
+    // coarse taps are monotone in the fine plane: the group spans [min taps(k), max taps(kl)]
+    const int kl = min(k + G, k1) - 1;
+    int iz[2];
+    T wz[2];
     itaps2<T>(k + gf.zoff, ncz, cz, iz, wz);
-    itaps2<T>(min(k + 1, kend - 1) + gf.zoff, ncz, cz, jz, vz2);
-    // coarse planes min(iz)..max(jz) not yet in the ring (even fine planes have taps
-    // {K, K-1}: not ordered, so ranges)
-    const int need_hi = max(max(iz[0], iz[1]), max(jz[0], jz[1]));
-    for (int c = max(min(iz[0], iz[1]), last + 1); c <= need_hi; ++c)
-      if (tid < CP) ring[(c & 3) * CP + tid] = coarse[gc.sz * (int64_t)(c - gc.zoff) + c_off];
-    last = max(last, need_hi);
-    const T xc = xn;
-    if (ADD && ok && k + 1 < k1) xn = fine[pxy + gf.sz * (int64_t)(k + 1)];
+    const int lo = max(min(iz[0], iz[1]), last + 1);
+    itaps2<T>(kl + gf.zoff, ncz, cz, iz, wz);
+    const int hi = max(iz[0], iz[1]);
+    T cv[SPAN];
+#pragma unroll
+    for (int q = 0; q < SPAN; ++q)
+      cv[q] = (lo + q <= hi) ? coarse[gc.sz * (int64_t)(lo + q - gc.zoff) + c_off] : T(0);
+    load_fine(k + G, xn);  // next group, in flight across this one
+#pragma unroll
+    for (int q = 0; q < SPAN; ++q)
+      if (lo + q <= hi && tid < CP) ring[((lo + q) & (NS - 1)) * CP + tid] = cv[q];
+    last = max(last, hi);
     __syncthreads();
-    T v = T(0);
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const T* pl = ring + (iz[c] & 3) * CP - cx0;
-      T vz = T(0);
+    for (int q = 0; q < G; ++q) {
+      const int kk = k + q;
+      if (kk > kl) break;
+      itaps2<T>(kk + gf.zoff, ncz, cz, iz, wz);
+      T v = T(0);
 #pragma unroll
-      for (int bq = 0; bq < 2; ++bq) {
-        const T* row = pl + (iy[bq] - cy0) * CXW;
-        vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
+      for (int c = 0; c < 2; ++c) {
+        const T* pl = ring + (iz[c] & (NS - 1)) * CP - cx0;
+        T vz = T(0);
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq) {
+          const T* row = pl + (iy[bq] - cy0) * CXW;
+          vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
+        }
+        v = fma(wz[c], vz, v);
       }
-      v = fma(wz[c], vz, v);
+      if (ok) {
+        const int64_t p = pxy + gf.sz * (int64_t)kk;
+        if (ADD) fine[p] = xc[q] + v;
+        else fine[p] = v;
+      }
     }
-    if (ok) {
-      const int64_t p = pxy + gf.sz * (int64_t)k;
-      if (ADD) fine[p] = xc + v;
-      else fine[p] = v;
-    }
-    __syncthreads();  // ring slots are reused two planes later
+    __syncthreads();  // ring slots are reused by the next group
+#pragma unroll
+    for (int q = 0; q < G; ++q) xc[q] = xn[q];
   }
 }
 

@@ -275,7 +275,15 @@ struct LevelData {
   uint32_t* sig = nullptr;
   uint32_t sig_epoch = 0;
 };
-constexpr int kBoundaryPlanes = 8;  // z-depth of a rank slab's boundary chunks (>= GHOST)
+// z-depth of a rank slab's boundary chunks (>= GHOST); MAD_BOUNDARY_PLANES overrides
+// it for tuning runs
+inline int boundary_planes() {
+  static const int v = [] {
+    const char* e = std::getenv("MAD_BOUNDARY_PLANES");
+    return e ? std::max(GHOST, std::atoi(e)) : 8;
+  }();
+  return v;
+}
 
 template <typename T>
 class Solver final : public SolverBase {
@@ -534,12 +542,16 @@ class Solver final : public SolverBase {
       flip = 1;
       sig = L.sig;
     } else if (part == 1) {  // the two boundary chunks of a rank slab (they produce the halo planes)
-      zr = ZRange{0, kBoundaryPlanes, nz - kBoundaryPlanes, 2};
+      zr = ZRange{0, boundary_planes(), nz - boundary_planes(), 2};
     } else if (part == 2) {  // the interior between them
-      const int ni = nz - 2 * kBoundaryPlanes;
-      int chunks = std::max(1, std::min((fc.blocks + tiles - 1) / tiles, std::max(1, ni / 16)));
+      const int ni = nz - 2 * boundary_planes();
+      static const int iblocks = [&] {
+        const char* e = std::getenv("MAD_INTERIOR_BLOCKS");  // tuning runs only
+        return e ? std::max(1, std::atoi(e)) : fc.blocks;
+      }();
+      int chunks = std::max(1, std::min((iblocks + tiles - 1) / tiles, std::max(1, ni / 16)));
       const int zc = (ni + chunks - 1) / chunks;
-      zr = ZRange{kBoundaryPlanes, zc, zc, (ni + zc - 1) / zc};
+      zr = ZRange{boundary_planes(), zc, zc, (ni + zc - 1) / zc};
     }
     const unsigned nb = (unsigned)(tiles * zr.nchunks);
     if (c_->d.gs_kernel == 2) {
@@ -639,7 +651,7 @@ class Solver final : public SolverBase {
       // rank slabs: which sweep form fused_sweep takes
       const LevelData<T>& L = lv_[l];
       if (c_->comm.active() && c_->geom[l].distributed && c_->d.gs_kernel != 2 &&
-          L.g.nz >= 3 * kBoundaryPlanes) {
+          L.g.nz >= 3 * boundary_planes()) {
         int tiles = 0, nchunks = 0;
         fused_shape(L, &tiles, &nchunks);
         const bool single = L.sig && nchunks >= 2;
@@ -690,7 +702,7 @@ class Solver final : public SolverBase {
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
     const bool dist = c_->comm.active() && c_->geom[l].distributed;
-    const bool overlap = dist && c_->d.gs_kernel != 2 && L.g.nz >= 3 * kBoundaryPlanes;
+    const bool overlap = dist && c_->d.gs_kernel != 2 && L.g.nz >= 3 * boundary_planes();
     int tiles = 0, nchunks = 0;
     if (overlap) fused_shape(L, &tiles, &nchunks);
     if (overlap && L.sig && nchunks >= 2) {
@@ -712,7 +724,7 @@ class Solver final : public SolverBase {
       // MAD_SPLIT_PROXY=1 (measurement only): launch a single-GPU slab as a rank slab's
       // boundary + interior parts, without the exchange (tools/bench_slab.py)
       static const bool proxy = std::getenv("MAD_SPLIT_PROXY") != nullptr;
-      if (proxy && c_->d.gs_kernel != 2 && L.g.nz >= 3 * kBoundaryPlanes) {
+      if (proxy && c_->d.gs_kernel != 2 && L.g.nz >= 3 * boundary_planes()) {
         launch_fused_part(L, 1);
         launch_fused_part(L, 2);
       } else {

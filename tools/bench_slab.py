@@ -12,7 +12,11 @@ def main():
     import multigridanisotropicdiffusion_amd as M
     out = []
     for nz in [int(v) for v in (sys.argv[1:] or ["512", "256", "128", "64"])]:
-        s = M.Solver((nz, 512, 512), time_step=0.1, smoother=M.GAUSS_SEIDEL)
+        # a middle rank of the 512^3 split (ghost planes on both sides, no transport:
+        # halos are skipped, the ghost planes hold zeros -- timing only)
+        nr = 512 // nz
+        s = M.Solver((nz, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, smoother=M.GAUSS_SEIDEL,
+                     nranks=nr, rank=min(1, nr - 1), global_shape=(512, 512, 512))
         s.synth_tensor(kind=0, seed=4)
         s.setup()
         s.synth_level(0, M.capi.B, 3)

@@ -1,0 +1,31 @@
+"""Run V-cycles of the bench workload for a kernel trace (per-level breakdown).
+    rocprofv3 --kernel-trace --output-format csv -d OUT -o vc -- python3 tools/vcycle_trace.py
+then   python tools/vcycle_breakdown.py OUT/vc_kernel_trace.csv"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--cycles", type=int, default=10)
+    a = p.parse_args()
+    import multigridanisotropicdiffusion_amd as M
+    S = a.size
+    s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32)
+    s.synth_tensor(kind=0, seed=4)
+    s.setup()
+    s.synth_level(0, M.capi.B, 3)
+    s.synth_level(0, M.capi.X, 3)
+    s.vcycle()
+    s.synchronize()
+    ms = s.bench_vcycle(a.cycles)
+    print(f"ms_per_vcycle {ms / a.cycles:.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
