@@ -134,6 +134,24 @@ __device__ __forceinline__ T resid_value(T b, T D, T u, T S) {
   return b - (Du - S);
 }
 
+// Gauss-Seidel point update u = (b + S) / D, shared by every GS kernel so they round
+// alike.  fp32: hardware reciprocal and one fma correction of the quotient (5 VALU
+// instead of the ~11 of the IEEE division sequence; within 1 ulp of the correctly
+// rounded quotient for the operator's D >= 1); fp64: IEEE division.
+template <typename T>
+__device__ __forceinline__ T gs_update(T b, T S, T D) {
+#pragma clang fp contract(off)
+  const T n = b + S;
+  if constexpr (sizeof(T) == 4) {
+    const float r = __builtin_amdgcn_rcpf(D);
+    const float q = n * r;
+    const float e = __builtin_fmaf(-q, D, n);
+    return __builtin_fmaf(e, r, q);
+  } else {
+    return n / D;
+  }
+}
+
 template <int DIM, int KIND>
 struct NbCount {
   static constexpr int N = (KIND == KFULL) ? (DIM == 3 ? 18 : 10) : (DIM == 3 ? 6 : 4);
@@ -219,7 +237,7 @@ __global__ void __launch_bounds__(256) gs_color_k(T* __restrict__ u, const T* __
   const int64_t p = i + g.sy * j + g.sz * k;
   T D, S;
   stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
-  u[p] = (b[p] + S) / D;
+  u[p] = gs_update(b[p], S, D);
 }
 
 // exact lexicographic GS (reference order, itkMultigridGaussSeidelSmoother.hxx:67-106)
@@ -237,7 +255,7 @@ __global__ void __launch_bounds__(256) gs_lex_plane_k(T* __restrict__ u, const T
   const int64_t p = i + g.sy * j + g.sz * k;
   T D, S;
   stencil_terms<T, DIM, KIND>(u, cf, g, rat, i, j, k, p, D, S);
-  u[p] = (b[p] + S) / D;
+  u[p] = gs_update(b[p], S, D);
 }
 
 // ---------------------------------------------------------------------------
@@ -539,7 +557,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
         const T bc = bv[c];
         T D, S;
         stencil_combine<T, 3, KIND>(q, nb, D, S);
-        P0[il] = (bc + S) / D;
+        P0[il] = gs_update(bc, S, D);
       }
       // this stage's registers are free: prefetch its data for the next step
       if (k + 1 <= kend) load_stage(c, k + 1);
@@ -619,6 +637,12 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   const int rx0 = txi * TX - H;
   const int ry0 = tyi * TY - H;
   const int tid = threadIdx.x;
+  // first thread of this wave (wave-uniform): a stage has fewer points than threads
+  // (665..512 of 1024 for the 64x32 tile), so whole waves sit a stage out -- they skip
+  // its loads and arithmetic instead of computing masked-off lanes, which leaves the
+  // SIMDs' issue slots to the waves that have points
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+  auto wave_in = [&](int c) { return wbase < FG::rows(c) * FG::cols(c); };
   const int nx = g.nx, ny = g.ny;
   const int sy = (int)g.sy, hx0 = g.hx0;
   // tile whose region keeps >= 2 points from every x/y face: no masks, no ghost images
@@ -789,7 +813,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   };
   auto stage = [&](int c, int k, int PM) {
     const int m = k - c;
-    if (!stage_on(c, m)) return;
+    if (!stage_on(c, m) || !wave_in(c)) return;
     const int zm = (m == 0 && !zlo_g) ? 1 : m - 1;
     const int zp = (m == g.nz - 1 && !zhi_g) ? g.nz - 2 : m + 1;
     const uint32_t o = pl[c][PM % NPM] + (uint32_t)(pdelta(c, PM).l * (int)TS);
@@ -832,7 +856,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     coefs_from_raw<T, 3, KIND>(raw[c], rat, q);
     T D, S;
     stencil_combine<T, 3, KIND>(q, nb, D, S);
-    const T v = ((BREC ? raw[c][NCF] : bv[c]) + S) / D;
+    const T v = gs_update(BREC ? raw[c][NCF] : bv[c], S, D);
     const int bit = c * 2 + PM;
     if (interior) {
       if (NC == 2 || FG::rows(c) * FG::cols(c) < NT) {
