@@ -683,25 +683,34 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
 
   auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
 
-  // Plane-load and output element offsets are recomputed every step from an opaque
-  // copy of the thread index (tq): keeping them resident costs 12 VGPRs, which
-  // pushes the kernel past 128 and into scratch spills that miss L2.
-  int tq = tid;
-  auto u_src = [&](int e) -> uint32_t {
-    const int q = tq + e * NT;
+  // Plane-load (source byte offset in a plane, LDS byte offset in a ring slot) and
+  // output (LDS, global) offsets of this thread's elements, computed once: recomputing
+  // them every step cost ~60 VALU per wave and step (integer division by RX, mirror),
+  // a quarter of the issue-bound sweep's vector instructions.  -1 marks no element.
+  uint32_t usrc[UPT];
+  int udst[UPT];
+#pragma unroll
+  for (int e = 0; e < UPT; ++e) {
+    const int q = tid + e * NT;
     const int lj = q / RX, li = q - (q / RX) * RX;
     int gi = rx0 + li, gj = ry0 + lj;
     if (!interior) {
       gi = mirror(gi, nx);
       gj = mirror(gj, ny);
     }
-    return (uint32_t)(gj * sy + gi) * TS;
-  };
-  auto u_dst = [&](int e) -> int {
-    const int q = tq + e * NT;
-    const int lj = q / RX, li = q - (q / RX) * RX;
-    return (q < RX * RY) ? (int)((lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS) : -1;
-  };
+    usrc[e] = (uint32_t)(gj * sy + gi) * TS;
+    udst[e] = (q < RX * RY) ? (int)((lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS) : -1;
+  }
+  int olds[OPT], oglb[OPT];
+#pragma unroll
+  for (int e = 0; e < OPT; ++e) {
+    const int q = tid + e * NT;
+    const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
+    const int gi = rx0 + li, gj = ry0 + lj;
+    const bool ok = q < TX * TY && gi < nx && gj < ny;
+    olds[e] = (int)((lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS);
+    oglb[e] = ok ? (int)((gj * sy + gi) * TS) : -1;
+  }
 
   // ---- stage points.  Stage c covers rows/cols of its colour in the region shrunk
   // by H - (NC-1-c) = c+1 on each side.  For plane parity PM:
@@ -782,16 +791,14 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     for (int e = 0; e < UPT; ++e) up[e] = T(0);
 #else
 #pragma unroll
-    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T, MAD_U_AUX>(rs, u_src(e), 0u);
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T, MAD_U_AUX>(rs, usrc[e], 0u);
 #endif
   };
   auto put_plane = [&](int m) {
     unsigned char* P = lbytes + slot(m) * (PLANE * TS);
 #pragma unroll
-    for (int e = 0; e < UPT; ++e) {
-      const int d = u_dst(e);
-      if (e < UPT - 1 || d >= 0) *reinterpret_cast<T*>(P + d) = up[e];
-    }
+    for (int e = 0; e < UPT; ++e)
+      if (e < UPT - 1 || udst[e] >= 0) *reinterpret_cast<T*>(P + udst[e]) = up[e];
   };
   // stage c data of step k (plane m = k - c, parity PM)
   // unconditional (the plane index clamped into the loadable range): a conditional
@@ -900,7 +907,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       if (k <= kend) {
         // keep the per-thread masks in VGPRs: without this the compiler hoists every
         // (stage, parity, flag) test out of the loop as a 64-bit lane mask and spills
-        asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(omask), "+v"(tq));
+        asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(omask));
         if (plane_ok(k + 1)) put_plane(k + 1);
         load_plane(k + 2);
         __syncthreads();
@@ -921,14 +928,9 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
           const unsigned char* P = lbytes + slot(mo) * (PLANE * TS);
           const __amdgpu_buffer_rsrc_t ro = buf_rsrc(uout + (int64_t)mo * sz);
 #pragma unroll
-          for (int e = 0; e < OPT; ++e) {
-            const int q = tq + e * NT;
-            const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
-            const int gi = rx0 + li, gj = ry0 + lj;
-            if (q < TX * TY && gi < nx && gj < ny)
-              buf_store<T, MAD_ST_AUX>(*reinterpret_cast<const T*>(P + (lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS),
-                           ro, (uint32_t)(gj * sy + gi) * TS);
-          }
+          for (int e = 0; e < OPT; ++e)
+            if (oglb[e] >= 0)
+              buf_store<T, MAD_ST_AUX>(*reinterpret_cast<const T*>(P + olds[e]), ro, (uint32_t)oglb[e]);
           if (signals && mo == GHOST - 1) {
             // the edge planes 0..GHOST-1 of this tile are stored: release them, count in
             __threadfence();
