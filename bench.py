@@ -115,7 +115,10 @@ def main():
     nz_local = S // world
     shape = (nz_local, S, S)
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
+    # SMOOTHER mode (the reference's CycleType 2: repeated sweeps of one system) -- the
+    # smoother-only protocol of SURVEY §8(d); level-0 records then carry b (mad_solver.hip)
     s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
+                 cycle=M.SMOOTHER,
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
                  gs_kernel=a.gs_kernel)
     if world > 1:

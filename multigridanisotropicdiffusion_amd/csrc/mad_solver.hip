@@ -334,7 +334,16 @@ class Solver final : public SolverBase {
       // coefficient records, point-interleaved (mad_kernels.hpp, cidx); 3D levels keep
       // GHOST coefficient planes per side: neighbour planes on rank slabs (the fused
       // sweep recomputes colours on them), padding for masked border lanes otherwise
-      L.brec = (dim == 3 && l == 0);
+      // Level 0's records carry b when b is reused by many sweeps: SMOOTHER mode (up to
+      // MaxCycles sweeps of one system per time step; the smoother benchmark) -- the
+      // sweeps run 3-6 % faster with one record stream.  V-cycle / FMG solves change b
+      // every time step after ~2 cycles (~12 level-0 record passes), where the 2.2 ms
+      // scatter of b into the 40-B records (partial-line writes, 512^3) costs more than
+      // it saves (VED diffusion 126 -> 116.5 ms without it, profiles/r01_brec_ab.log).
+      // MAD_BREC=0/1 overrides (A/B runs).
+      bool brec_on = c->d.cycle == MAD_SMOOTHER;
+      if (const char* e = std::getenv("MAD_BREC")) brec_on = e[0] != '0';
+      L.brec = (dim == 3 && l == 0 && brec_on);
       L.g.rs = ncoef_ + (L.brec ? 1 : 0);
       const int64_t cplane = L.g.sz * L.g.rs;
       const int64_t cgp = (dim == 3) ? GHOST : 0;

@@ -32,8 +32,10 @@ def _multi(nranks, fn, T, **kw):
 
 
 @pytest.mark.parametrize("nranks", [2, 4])
-@pytest.mark.parametrize("smoother,gs_kernel", [(0, 0), (0, 1), (2, 0), (0, 3)])
-def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel):
+@pytest.mark.parametrize("smoother,gs_kernel,cycle", [(0, 0, 0), (0, 1, 0), (2, 0, 0), (0, 3, 0),
+                                                      (0, 3, 2)])
+def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle):
+    """cycle 2 (SMOOTHER): level-0 records carry b (sync_brec on ghost planes)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     T = synth.random_spd(SHAPE, seed=3)
@@ -51,7 +53,7 @@ def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel):
         s.vcycle()
         v = s.download(0, M.capi.X)
         return a, v, s.residual(0)
-    kw = dict(smoother=smoother, gs_kernel=gs_kernel)
+    kw = dict(smoother=smoother, gs_kernel=gs_kernel, cycle=cycle)
     ref = _single(fn, T, **kw)
     out = _multi(nranks, fn, T, **kw)
     np.testing.assert_array_equal(np.concatenate([o[0] for o in out]), ref[0])
@@ -81,7 +83,8 @@ def test_distributed_filter_run_matches_single(nranks):
 
 @pytest.mark.parametrize("nranks", [2])
 @pytest.mark.parametrize("gs_kernel", [4])
-def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel):
+@pytest.mark.parametrize("cycle", [0, 2])
+def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel, cycle):
     """gs_kernel 4 on rank slabs deep enough for two z-chunks per tile column (64 planes
     per rank): the single-launch sweep -- the top chunk marches downward, the edge chunks
     signal their finished edge planes and the communication stream exchanges them while
@@ -108,7 +111,7 @@ def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel):
     def single(_, s):
         return fn(None, s)
 
-    s = M.Solver(shape, time_step=0.4, gs_kernel=gs_kernel)
+    s = M.Solver(shape, time_step=0.4, gs_kernel=gs_kernel, cycle=cycle)
     s.set_tensor(T)
     s.setup()
     ref = single(None, s)
@@ -117,6 +120,6 @@ def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel):
         s.set_tensor(T)
         s.setup()
         return fn(r, s)
-    out = D.run_local(nranks, body, shape, time_step=0.4, gs_kernel=gs_kernel)
+    out = D.run_local(nranks, body, shape, time_step=0.4, gs_kernel=gs_kernel, cycle=cycle)
     np.testing.assert_array_equal(np.concatenate([o[0] for o in out]), ref[0])
     np.testing.assert_array_equal(np.concatenate([o[1] for o in out]), ref[1])

@@ -177,7 +177,8 @@ def test_converged_solution_matches_reference_gs(name, prec):
     ((6, 3, 9), "full"), ((130, 66, 24), "full"), ((4, 4, 4), "iso"), ((3, 24, 20), "full"),
     ((40, 3, 16), "diag"), ((18, 20, 3), "iso"), ((70, 16, 3), "full"),
 ])
-def test_fused_gs_sweep_is_bitwise_per_colour_passes(shape, tensor, prec):
+@pytest.mark.parametrize("cycle", [0, 2])  # 2 (SMOOTHER): level-0 records carry b
+def test_fused_gs_sweep_is_bitwise_per_colour_passes(shape, tensor, prec, cycle):
     """The single-launch fused sweeps (gs_fused_k v2 and gs_fused3_k v3: z-wavefront,
     overlapped tiles, z-chunks; v3 with mirror ghosts in LDS) equal NC in-place
     colour passes bit for bit, including partial tiles, partial z-chunks, odd sizes
@@ -190,7 +191,8 @@ def test_fused_gs_sweep_is_bitwise_per_colour_passes(shape, tensor, prec):
          "iso": lambda: synth.isotropic(shape)}[tensor]()
     outs = []
     for variant in (1, 2, 3, 4):  # 4: v3 with the last z-chunk marched downward
-        s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec, gs_kernel=variant)
+        s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec, gs_kernel=variant,
+                     cycle=cycle)
         s.set_tensor(T)
         s.setup()
         s.upload(0, M.capi.X, synth.image(shape, seed=4))

@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 def main():
     import multigridanisotropicdiffusion_amd as M
     shape = (512, 1024, 1024)  # (z, y, x)
-    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32)
+    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=M.SMOOTHER)
     t0 = time.perf_counter()
     s.synth_tensor(kind=0, seed=5)
     s.setup()

@@ -20,7 +20,7 @@ def main():
     import multigridanisotropicdiffusion_amd as M
     S = a.size
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
-    s = M.Solver((S, S, S), time_step=0.1, smoother=sm, gs_kernel=a.gs_kernel)
+    s = M.Solver((S, S, S), time_step=0.1, smoother=sm, gs_kernel=a.gs_kernel, cycle=M.SMOOTHER)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     out = []

@@ -52,9 +52,9 @@ def main():
             return None
 
         if n == 1:
-            body(0, M.Solver((S, S, S), time_step=0.1))
+            body(0, M.Solver((S, S, S), time_step=0.1, cycle=M.SMOOTHER))
         else:
-            D.run_local(n, body, (S, S, S), time_step=0.1)
+            D.run_local(n, body, (S, S, S), time_step=0.1, cycle=M.SMOOTHER)
         wall = max(v[0] for v in res.values())
         vwall = max(v[2] for v in res.values())
         print(json.dumps({"ranks": n, "slab": list(res[0][3]),

@@ -16,6 +16,7 @@ def main():
         # halos are skipped, the ghost planes hold zeros -- timing only)
         nr = 512 // nz
         s = M.Solver((nz, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, smoother=M.GAUSS_SEIDEL,
+                     cycle=M.SMOOTHER,
                      nranks=nr, rank=min(1, nr - 1), global_shape=(512, 512, 512))
         s.synth_tensor(kind=0, seed=4)
         s.setup()

@@ -27,7 +27,8 @@ def main():
     import multigridanisotropicdiffusion_amd as M
     S = a.size
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
-    s = M.Solver((S, S, S), time_step=0.1, smoother=sm, gs_kernel=a.gs_kernel)
+    s = M.Solver((S, S, S), time_step=0.1, smoother=sm, gs_kernel=a.gs_kernel,
+                 cycle=M.SMOOTHER)  # the bench's configuration
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)

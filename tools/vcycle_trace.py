@@ -16,7 +16,7 @@ def main():
     a = p.parse_args()
     import multigridanisotropicdiffusion_amd as M
     S = a.size
-    s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32)
+    s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32, cycle=M.SMOOTHER)  # as bench.py
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
