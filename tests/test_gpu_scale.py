@@ -1,0 +1,98 @@
+"""Full-size GPU checks at BASELINE.json's C4 (512^3) and C5 (1024 x 1024 x 512) shapes,
+through size-independent properties (the oracle does not finish at these sizes):
+
+  - the fused single-launch sweep equals NC per-colour passes bit for bit (the per-colour
+    kernel is checked against the oracle at small sizes, tests/test_gpu_kernels.py);
+  - A 1 = 1 (row sums): a constant rhs and guess stay constant under sweeps;
+  - V-cycles cut the residual by a mesh-independent factor (C5).
+
+Plus SMOOTHER mode (CycleType 2, the reference's smoother-only solve) through mad_run against
+the oracle, with the level-0 records carrying b (the smoother benchmark's layout)."""
+import numpy as np
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def M():
+    import multigridanisotropicdiffusion_amd as M
+    return M
+
+
+@pytest.mark.parametrize("gs_kernel", [0, 3])
+@pytest.mark.parametrize("precision,tol", [("FP32", 1e-5), ("FP64", 1e-9)])
+def test_smoother_mode_run_matches_oracle(M, oracle_mod, gs_kernel, precision, tol):
+    """GenerateData with CycleType SMOOTHER (itkMultigridAnisotropicDiffusionImageFilter.hxx:
+    170-246): repeated level-0 sweeps until relres <= tolerance.  Multicolour GS on the GPU,
+    lexicographic GS in the oracle: both converge to the same solution."""
+    shape = (24, 26, 28)
+    T = synth.random_spd(shape, seed=21)
+    x = synth.image(shape, seed=22)
+    o = oracle_mod.Oracle(shape, (1.0, 0.9, 1.1), T, 0.1)
+    ref, _, rr = o.run(x, tolerance=1e-11, cycle=oracle_mod.SMOOTHER, max_cycles=400)
+    assert rr[-1] <= 1e-11
+    s = M.Solver(shape, (1.0, 0.9, 1.1), time_step=0.1, cycle=M.SMOOTHER, max_cycles=400,
+                 tolerance=1e-11 if precision == "FP64" else 1e-7,
+                 precision=getattr(M, precision), gs_kernel=gs_kernel)
+    s.set_tensor(T)
+    out, st = s.run(x, out_dtype=np.float64)
+    assert np.abs(out - ref).max() / np.abs(ref).max() < tol
+
+
+def _c4(M, gs_kernel, cycle):
+    s = M.Solver((512, 512, 512), time_step=0.1, precision=M.FP32, cycle=cycle,
+                 gs_kernel=gs_kernel)
+    s.synth_tensor(kind=0, seed=4)
+    s.setup()
+    return s
+
+
+def test_c4_512_fused_sweep_equals_per_colour_passes(M):
+    """C4 shape, VED-form full tensor, level-0 records carrying b (SMOOTHER): two fused
+    sweeps (the bench kernel) == two sweeps of four per-colour launches, bit for bit."""
+    outs = []
+    for gs_kernel in (0, 1):
+        s = _c4(M, gs_kernel, M.SMOOTHER)
+        s.synth_level(0, M.capi.B, 3)
+        s.synth_level(0, M.capi.X, 5)
+        s.smooth(0, 2)
+        outs.append(s.download(0, M.capi.X).astype(np.float32))
+        if gs_kernel == 0:
+            assert "gs_fused3_k" in s.smooth_kernel_name(0) and "true" in s.smooth_kernel_name(0)
+        s.close()
+    assert np.array_equal(outs[0], outs[1]), np.abs(outs[0] - outs[1]).max()
+
+
+def test_c4_512_constant_is_a_fixed_point(M):
+    """Row sums are 1 on the DCA operator (A 1 = 1): b = x = 1 stays 1 under the fused
+    sweeps and the residual is at the fp32 rounding level, at the full C4 size."""
+    s = _c4(M, 0, M.SMOOTHER)
+    s.fill(0, M.capi.B, 1.0)
+    s.fill(0, M.capi.X, 1.0)
+    s.smooth(0, 3)
+    assert s.residual(0) / s.norm(0, M.capi.B) < 1e-6
+    x = s.download(0, M.capi.X)
+    assert np.abs(x - 1.0).max() < 1e-5
+    s.close()
+
+
+def test_c5_vcycle_convergence_factor(M):
+    """C5 shape (1024 x 1024 x 512, 537 M voxels) on one GPU: every V-cycle above the fp32
+    floor cuts the residual by a mesh-independent factor (same bound as at 256^3)."""
+    s = M.Solver((512, 1024, 1024), time_step=0.1, precision=M.FP32)
+    s.synth_tensor(kind=0, seed=5)
+    s.setup()
+    assert s.num_levels == 7
+    s.synth_level(0, M.capi.B, 5)
+    s.synth_level(0, M.capi.X, 9)
+    bn = s.norm(0, M.capi.B)
+    rel = [s.residual(0) / bn]
+    for _ in range(3):
+        s.vcycle()
+        rel.append(s.residual(0) / bn)
+    factors = [b / a for a, b in zip(rel, rel[1:]) if b > 1e-6]
+    assert factors and max(factors) < 0.2, rel
+    s.close()
