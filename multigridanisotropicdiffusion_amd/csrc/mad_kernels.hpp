@@ -1546,11 +1546,31 @@ __device__ __forceinline__ double delta_f(const double* __restrict__ f, int64_t 
   return f[p + st] - f[p - st];
 }
 
+// spacing / time-step factors of the coefficient fields, computed once on the host
+// (the kernel then multiplies instead of dividing: fp64 division is a long VALU sequence)
+struct CoefFactors {
+  double fa[3];      // dt / h_d^2                 (a_d = fa[d] M_dd)
+  double fg[3];      // 1 / (2 h_d2)               (g_d = fgo[d] sum_d2 delta_d2 M_d,d2 fg[d2])
+  double fgo[3];     // dt / (2 h_d)
+  double fe[3][3];   // dt / (2 h_d h_d2)          (e_dd2 = fe[d][d2] M_d,d2)
+};
+
+inline CoefFactors coef_factors(const double h[3], double dt) {
+  CoefFactors f{};
+  for (int d = 0; d < 3; ++d) {
+    f.fa[d] = dt / (h[d] * h[d]);
+    f.fg[d] = 1.0 / (2.0 * h[d]);
+    f.fgo[d] = dt / (2.0 * h[d]);
+    for (int d2 = 0; d2 < 3; ++d2) f.fe[d][d2] = dt / (2.0 * h[d] * h[d2]);
+  }
+  return f;
+}
+
 // coefficient fields of one (global) level from its fp64 tensor
 template <typename T, int DIM, int KIND>
 __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M, int nx, int ny,
-                                                    int nz, double hx, double hy, double hz,
-                                                    double dt, T* __restrict__ cf, int rs) {
+                                                    int nz, CoefFactors f, T* __restrict__ cf,
+                                                    int rs) {
   using L = CoefLayout<DIM, KIND>;
   const int k = (DIM == 3) ? (int)blockIdx.z : 0;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
@@ -1560,26 +1580,30 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
   const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
   // output record in the point-interleaved, x-parity-split coefficient layout (cidx)
   const int64_t o = ((int64_t)nx * (j + (int64_t)ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * rs;
-  const double h[3] = {hx, hy, hz};
   const int nn[3] = {nx, ny, nz};
   const int id[3] = {i, j, k};
   const int64_t st[3] = {1, nx, (int64_t)nx * ny};
   if (KIND == KISO) {
-    cf[o] = (T)(dt * M[p] / (h[0] * h[0]));
+    cf[o] = (T)(f.fa[0] * M[p]);
   } else {
-    for (int d = 0; d < DIM; ++d) cf[o + d] = (T)(dt * M[tcomp(DIM, d, d) * n + p] / (h[d] * h[d]));
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) cf[o + d] = (T)(f.fa[d] * M[tcomp(DIM, d, d) * n + p]);
   }
+#pragma unroll
   for (int d = 0; d < DIM; ++d) {
     double s = 0.0;
+#pragma unroll
     for (int d2 = 0; d2 < DIM; ++d2)
-      s += delta_f(M + tcomp(DIM, d, d2) * n, p, id[d2], nn[d2], st[d2]) / (2.0 * h[d2]);
-    cf[o + L::NA + d] = (T)(dt / (2.0 * h[d]) * s);
+      s += delta_f(M + tcomp(DIM, d, d2) * n, p, id[d2], nn[d2], st[d2]) * f.fg[d2];
+    cf[o + L::NA + d] = (T)(f.fgo[d] * s);
   }
   if (KIND == KFULL) {
     int e = L::NA + L::NG;
+#pragma unroll
     for (int d = 0; d < DIM; ++d)
+#pragma unroll
       for (int d2 = d + 1; d2 < DIM; ++d2, ++e)
-        cf[o + e] = (T)(dt * M[tcomp(DIM, d, d2) * n + p] / (2.0 * h[d] * h[d2]));
+        cf[o + e] = (T)(f.fe[d][d2] * M[tcomp(DIM, d, d2) * n + p]);
   }
 }
 

@@ -565,7 +565,7 @@ class Solver final : public SolverBase {
     const unsigned nb = (unsigned)(tiles * zr.nchunks);
     if (c_->d.gs_kernel == 2) {
       REQUIRE(part == 0, MAD_ERR_UNSUPPORTED, "fused v2 sweeps the whole slab");
-      hipLaunchKernelGGL((gs_fused_k<T, KD, 64, 16, (KD == KFULL ? 512 : 1024), 4>),
+      hipLaunchKernelGGL((gs_fused_k<T, KD, 64, 16, (KD == KFULL ? 512 : 1024), (sizeof(T) == 8 ? 2 : 4)>),
                          dim3((unsigned)(((L.g.nx + 63) / 64) * ((L.g.ny + 15) / 16) * zr.nchunks)),
                          dim3(KD == KFULL ? 512 : 1024), 0, c_->stream, L.x, L.t, L.b, L.cf, L.g,
                          L.rat, zr.zc, (L.g.nx + 63) / 64, (L.g.ny + 15) / 16);
@@ -643,8 +643,8 @@ class Solver final : public SolverBase {
     } else if (!use_fused(l)) {
       std::snprintf(buf, sizeof buf, "gs_color_k<%s, %d, %d>", tn, dim, kind);
     } else if (c_->d.gs_kernel == 2) {
-      std::snprintf(buf, sizeof buf, "gs_fused_k<%s, %d, 64, 16, %d, 4>", tn, kind,
-                    kind == KFULL ? 512 : 1024);
+      std::snprintf(buf, sizeof buf, "gs_fused_k<%s, %d, 64, 16, %d, %d>", tn, kind,
+                    kind == KFULL ? 512 : 1024, sizeof(T) == 8 ? 2 : 4);
     } else {
       const FusedCfg& fc = fused_cfg();
       int tx = 64, ty = 16, nt = kind == KFULL ? 512 : 1024;
@@ -1373,11 +1373,19 @@ class Solver final : public SolverBase {
         gc.sy = G.n[0]; gc.sz = G.n[0] * G.n[1]; gc.N = Ng;
         dim3 gr = grid_for(gc.nx, gc.ny, gc.nz, BLK);
         for (int k = 0; k < ncomp; ++k) {
-          if (dim == 3)
-            hipLaunchKernelGGL((restrict_k<double, double, 3>), gr, BLK, 0, c_->stream,
+          if (dim == 3) {
+            // z-marching restriction (LDS-staged planes; same taps and fma order as
+            // restrict_k, bit-identical), ~1024 blocks
+            constexpr int CX = 32, CY = 8;
+            const int ntx = (gc.nx + CX - 1) / CX, nty = (gc.ny + CY - 1) / CY;
+            int chunks = std::max(1, std::min((1024 + ntx * nty - 1) / (ntx * nty), gc.nz / 4));
+            const int kc = (gc.nz + chunks - 1) / chunks;
+            chunks = (gc.nz + kc - 1) / kc;
+            hipLaunchKernelGGL((restrict3_k<double, double, CX, CY>),
+                               dim3((unsigned)(ntx * nty * chunks)), dim3(CX * CY), 0, c_->stream,
                                fine + k * Gf.N, gf, coarse + k * Ng, gc, G.cent[0], G.cent[1],
-                               G.cent[2], 0);
-          else
+                               G.cent[2], 0, gc.nz, kc, ntx);
+          } else
             hipLaunchKernelGGL((restrict_k<double, double, 2>), gr, BLK, 0, c_->stream,
                                fine + k * Gf.N, gf, coarse + k * Ng, gc, G.cent[0], G.cent[1],
                                G.cent[2], 0);
@@ -1400,8 +1408,8 @@ class Solver final : public SolverBase {
       dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
       dispatch(dim, c_->kind, [&](auto D, auto K) {
         hipLaunchKernelGGL((build_coef_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
-                           (int)G.n[0], (int)G.n[1], (int)G.n[2], G.h[0], G.h[1], G.h[2],
-                           c_->d.time_step, dst, L.g.rs);
+                           (int)G.n[0], (int)G.n[1], (int)G.n[2],
+                           coef_factors(G.h, c_->d.time_step), dst, L.g.rs);
       });
       HIP_CHECK(hipGetLastError());
       if (slab) {
@@ -1433,8 +1441,8 @@ class Solver final : public SolverBase {
     dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
     dispatch(dim, c_->kind, [&](auto D, auto K) {
       hipLaunchKernelGGL((build_coef_k<double, D.value, K.value>), gr, BLK, 0, c_->stream,
-                         tensor_l, (int)G.n[0], (int)G.n[1], (int)G.n[2], G.h[0], G.h[1], G.h[2],
-                         c_->d.time_step, cf64, nc);
+                         tensor_l, (int)G.n[0], (int)G.n[1], (int)G.n[2],
+                         coef_factors(G.h, c_->d.time_step), cf64, nc);
     });
     HIP_CHECK(hipGetLastError());
     coarse_coef64_.resize((size_t)G.N * nc);
