@@ -226,6 +226,77 @@ __device__ inline void sym3_eigen(E a00, E a01, E a02, E a11, E a12, E a22, E w[
   sw(0, 1);
 }
 
+// fp32 mode's eigen-analysis: closed-form (trigonometric) eigenvalues of the symmetric 3x3
+// matrix, evaluated in fp64 -- the acos of the normalised determinant loses half the digits
+// when two eigenvalues cluster (error ~ sqrt(eps) of the spread), which fp32 cannot afford
+// (measured: tensor errors 3e-3 against the oracle) and fp64 can (~1e-8).  Ascending in w;
+// diagonal input returns the diagonal in the order sym3_eigen's ascending sort produces.
+__device__ inline void sym3_eigvals_closed(double a00, double a01, double a02, double a11,
+                                           double a12, double a22, double w[3], double& spread) {
+#pragma clang fp contract(off)
+  const double p1 = a01 * a01 + a02 * a02 + a12 * a12;
+  const double q = (a00 + a11 + a22) * (1.0 / 3.0);
+  const double b00 = a00 - q, b11 = a11 - q, b22 = a22 - q;
+  const double p2 = b00 * b00 + b11 * b11 + b22 * b22 + 2.0 * p1;
+  const double p = sqrt(p2 * (1.0 / 6.0));
+  spread = p;
+  if (!(p > 0.0) || p1 == 0.0) {  // diagonal (or a multiple of I): sort the diagonal
+    double d0 = a00, d1 = a11, d2 = a22, t;
+    if (d0 > d1) { t = d0; d0 = d1; d1 = t; }
+    if (d1 > d2) { t = d1; d1 = d2; d2 = t; }
+    if (d0 > d1) { t = d0; d0 = d1; d1 = t; }
+    w[0] = d0; w[1] = d1; w[2] = d2;
+    return;
+  }
+  const double ip = 1.0 / p;
+  const double c00 = b00 * ip, c11 = b11 * ip, c22 = b22 * ip;
+  const double c01 = a01 * ip, c02 = a02 * ip, c12 = a12 * ip;
+  const double det = c00 * (c11 * c22 - c12 * c12) - c01 * (c01 * c22 - c12 * c02) +
+                     c02 * (c01 * c12 - c11 * c02);
+  const double r = fmin(fmax(0.5 * det, -1.0), 1.0);
+  const double phi = acos(r) * (1.0 / 3.0);
+  const double hi = q + 2.0 * p * cos(phi);
+  const double lo = q + 2.0 * p * cos(phi + 2.0943951023931957);  // + 2 pi / 3
+  w[2] = hi;
+  w[0] = lo;
+  w[1] = 3.0 * q - hi - lo;
+}
+
+// unit eigenvector of eigenvalue lam (fp64): the largest cross product of two rows of
+// A - lam I.  Returns false when lam is within 1e-3 of the spread from another eigenvalue
+// (the caller then falls back to the Jacobi iteration for this voxel).
+__device__ inline bool sym3_eigvec_closed(double a00, double a01, double a02, double a11,
+                                          double a12, double a22, double lam, double gap,
+                                          double spread, double v[3]) {
+#pragma clang fp contract(off)
+  if (!(gap > 1e-3 * spread)) return false;
+  const double r0[3] = {a00 - lam, a01, a02};
+  const double r1[3] = {a01, a11 - lam, a12};
+  const double r2[3] = {a02, a12, a22 - lam};
+  auto cross = [](const double* x, const double* y, double* z) {
+    z[0] = x[1] * y[2] - x[2] * y[1];
+    z[1] = x[2] * y[0] - x[0] * y[2];
+    z[2] = x[0] * y[1] - x[1] * y[0];
+  };
+  double c0[3], c1[3], c2[3];
+  cross(r0, r1, c0);
+  cross(r0, r2, c1);
+  cross(r1, r2, c2);
+  const double n0 = c0[0] * c0[0] + c0[1] * c0[1] + c0[2] * c0[2];
+  const double n1 = c1[0] * c1[0] + c1[1] * c1[1] + c1[2] * c1[2];
+  const double n2 = c2[0] * c2[0] + c2[1] * c2[1] + c2[2] * c2[2];
+  const double* c = c0;
+  double n = n0;
+  if (n1 > n) { c = c1; n = n1; }
+  if (n2 > n) { c = c2; n = n2; }
+  if (!(n > 0.0)) return false;
+  const double in = 1.0 / sqrt(n);
+  v[0] = c[0] * in;
+  v[1] = c[1] * in;
+  v[2] = c[2] * in;
+  return true;
+}
+
 // VesselnessFunction (VED.hxx:176-212) on eigenvalues sorted by magnitude, in E; the
 // reference's unqualified abs() on doubles is fabs.
 template <typename E>
@@ -306,9 +377,19 @@ __global__ void __launch_bounds__(256) ved_fir_x_k(const T* __restrict__ a00, co
     return;
   }
   // eigen-analysis and vesselness in the storage precision T (fp64 = the reference's
-  // Precision; fp32 in the fp32 mode, like the solver)
+  // Precision, cyclic Jacobi; fp32 in the fp32 mode, like the solver: closed-form
+  // eigenvalues, and the eigenvector -- only where this scale's response wins -- from
+  // cross products, with the Jacobi iteration as the fallback for near-degenerate cases)
+  const T A0 = (T)H0, A1 = (T)H1, A2 = (T)H2, A3 = (T)H3, A4 = (T)H4, A5 = (T)H5;
   T w[3], V[3][3];
-  sym3_eigen<T>((T)H0, (T)H1, (T)H2, (T)H3, (T)H4, (T)H5, w, V);
+  double wd[3], spread = 0.0;
+  if constexpr (sizeof(T) == 4) {
+    // the fp32 Hessian components, widened: the closed form runs in fp64
+    sym3_eigvals_closed(A0, A1, A2, A3, A4, A5, wd, spread);
+    w[0] = (T)wd[0]; w[1] = (T)wd[1]; w[2] = (T)wd[2];
+  } else {
+    sym3_eigen<T>(A0, A1, A2, A3, A4, A5, w, V);
+  }
   // sort by magnitude with the reference's three swaps (VED.hxx:266-268)
   T e0 = w[0], e1 = w[1], e2 = w[2], tt;
   if (fabs(e0) > fabs(e1)) { tt = e0; e0 = e1; e1 = tt; }
@@ -316,10 +397,22 @@ __global__ void __launch_bounds__(256) ved_fir_x_k(const T* __restrict__ a00, co
   if (fabs(e0) > fabs(e1)) { tt = e0; e0 = e1; e1 = tt; }
   const double v = (double)ved_vesselness<T>(e0, e1, e2, vp);
   if (first || v > resp[p]) {
+    T d[3];
+    if constexpr (sizeof(T) == 4) {
+      double dd[3];
+      if (sym3_eigvec_closed(A0, A1, A2, A3, A4, A5, wd[2], wd[2] - wd[1], spread, dd)) {
+        d[0] = (T)dd[0]; d[1] = (T)dd[1]; d[2] = (T)dd[2];
+      } else {
+        sym3_eigen<T>(A0, A1, A2, A3, A4, A5, w, V);
+        d[0] = V[0][2]; d[1] = V[1][2]; d[2] = V[2][2];
+      }
+    } else {
+      d[0] = V[0][2]; d[1] = V[1][2]; d[2] = V[2][2];
+    }
     resp[p] = v;
-    dir[p] = (double)V[0][2];
-    dir[n + p] = (double)V[1][2];
-    dir[2 * n + p] = (double)V[2][2];
+    dir[p] = (double)d[0];
+    dir[n + p] = (double)d[1];
+    dir[2 * n + p] = (double)d[2];
   }
 }
 
