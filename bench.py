@@ -105,6 +105,10 @@ def main():
     n_gpus = max(a.gpus, world)
     dist = None
     if world > 1:
+        # one node (the contract launches --nnodes=1): RCCL's bootstrap stays on loopback,
+        # the halos go GPU to GPU over xGMI
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_DEBUG", "WARN")
         import torch  # noqa: F401  (torch first: our library then binds to the same HIP runtime)
         import torch.distributed as dist
         dist.init_process_group("gloo")
