@@ -150,6 +150,7 @@ def main():
     dev_ms, kern_ms, launches = s.bench_smooth(0, a.steps)
     barrier()
     wall = time.perf_counter() - t0
+    per_launch = sorted(s.bench_launch_times())
     if dist is not None:
         import torch
         tt = torch.tensor([wall], dtype=torch.float64)
@@ -189,6 +190,8 @@ def main():
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": kname,
             "kernel_ms_mean": round(kern_ms, 5), "launches": launches,
+            "kernel_ms_median": round(per_launch[len(per_launch) // 2], 5) if per_launch else None,
+            "kernel_ms_min": round(per_launch[0], 5) if per_launch else None,
             "algorithmic_bytes_per_launch": BYTES_PER_VOXEL_SMOOTH * units_per_launch}
     if traffic:
         roof["traffic_source"] = traffic.get("source")

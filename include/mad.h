@@ -201,6 +201,10 @@ int mad_synchronize(mad_ctx *ctx);
  * (sweep) kernel launches.  Used by bench.py. */
 int mad_bench_smooth(mad_ctx *ctx, int32_t level, uint32_t sweeps, double *total_ms,
                      double *kernel_ms_mean, uint32_t *kernel_launches);
+/* Per-launch durations (ms, HIP events) of the dominant kernel in the last
+ * mad_bench_smooth call: up to `cap` values into `ms`, their count into *n
+ * (median / min for the SURVEY 8(d) timing protocol). */
+int mad_bench_launch_times(mad_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
 /* Name of the kernel one smoother sweep on `level` launches, as rocprofv3 prints
  * its template arguments (e.g. "gs_fused3_k<float, 3, 64, 32, 1024, 4, 2>"), so a
  * profile summary can be matched to the bench line. */

@@ -35,7 +35,7 @@ EXPORTS = (
     "mad_level_info", "mad_upload",
     "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
     "mad_interpolate", "mad_prolongate_add", "mad_coarse_solve", "mad_vcycle", "mad_fmg",
-    "mad_synchronize", "mad_bench_smooth", "mad_smooth_kernel_name", "mad_bench_vcycle", "mad_bench_synth_tensor",
+    "mad_synchronize", "mad_bench_smooth", "mad_bench_launch_times", "mad_smooth_kernel_name", "mad_bench_vcycle", "mad_bench_synth_tensor",
     "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_comm_init_local",
     "mad_slab_range",
     # include/mad_ved.h
@@ -194,6 +194,7 @@ def load():
         "mad_fmg": ([vp], i32),
         "mad_synchronize": ([vp], i32),
         "mad_bench_smooth": ([vp, i32, u32, dp, dp, u32p], i32),
+        "mad_bench_launch_times": ([vp, ctypes.POINTER(ctypes.c_float), u32, u32p], i32),
         "mad_smooth_kernel_name": ([vp, i32, ctypes.c_char_p, i32], i32),
         "mad_bench_vcycle": ([vp, u32, dp], i32),
         "mad_bench_synth_tensor": ([vp, i32, ctypes.c_uint64], i32),

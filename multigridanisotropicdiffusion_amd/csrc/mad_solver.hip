@@ -229,6 +229,7 @@ struct SolverBase {
                    mad_stats* st) = 0;
   virtual void bench_smooth(int l, unsigned n, double* total_ms, double* kern_ms,
                             unsigned* launches) = 0;
+  std::vector<float> launch_ms;  // per-launch durations of the last bench_smooth
   virtual void bench_vcycle(unsigned n, double* total_ms) = 0;
   virtual void synth_level(int l, int which, uint64_t seed) = 0;
   virtual std::string smooth_kernel(int l) = 0;
@@ -1260,10 +1261,12 @@ class Solver final : public SolverBase {
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, a, z));
     double ksum = 0.0;
+    launch_ms.assign(q, 0.f);
     for (unsigned i = 0; i < q; ++i) {
       float km = 0.f;
       HIP_CHECK(hipEventElapsedTime(&km, ev[2 * i], ev[2 * i + 1]));
       ksum += km;
+      launch_ms[i] = km;
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
     (void)hipEventDestroy(a);
@@ -2037,6 +2040,14 @@ int mad_bench_smooth(mad_ctx* c, int32_t level, uint32_t sweeps, double* total_m
                REQUIRE(total_ms && kernel_ms_mean && kernel_launches, MAD_ERR_INVALID, "null out");
                unsigned nl = 0; c->solver->bench_smooth(level, sweeps, total_ms, kernel_ms_mean, &nl);
                *kernel_launches = nl);
+}
+
+int mad_bench_launch_times(mad_ctx* c, float* ms, uint32_t cap, uint32_t* n) {
+  KERNEL_ENTRY(REQUIRE(n && (ms || cap == 0), MAD_ERR_INVALID, "null out");
+               const std::vector<float>& v = c->solver->launch_ms;
+               const uint32_t k = std::min<uint32_t>(cap, (uint32_t)v.size());
+               for (uint32_t i = 0; i < k; ++i) ms[i] = v[i];
+               *n = k);
 }
 
 int mad_smooth_kernel_name(mad_ctx* c, int32_t level, char* buf, int32_t len) {

@@ -226,6 +226,13 @@ class Solver:
                                              ctypes.byref(k), ctypes.byref(n)))
         return t.value, k.value, n.value
 
+    def bench_launch_times(self):
+        """Per-launch kernel durations (ms) of the last bench_smooth."""
+        buf = (ctypes.c_float * 4096)()
+        n = ctypes.c_uint32()
+        self._check(self._L.mad_bench_launch_times(self._ctx, buf, 4096, ctypes.byref(n)))
+        return list(buf[:n.value])
+
     def smooth_kernel_name(self, level=0):
         buf = ctypes.create_string_buffer(256)
         self._check(self._L.mad_smooth_kernel_name(self._ctx, level, buf, 256))
