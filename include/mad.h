@@ -227,6 +227,11 @@ int mad_comm_init(mad_ctx *ctx, const void *uid128);
  * ghost planes by device-to-device copies.  Same bytes as the RCCL path; used to
  * test the z-slab decomposition on a single GPU. */
 int mad_comm_init_local(mad_ctx *ctx, uint64_t group);
+/* Transport self-test on one GPU: a single-rank RCCL communicator runs the halo
+ * exchange (grouped ncclSend/ncclRecv, both neighbours = this rank), the fp64
+ * allreduce and the slab allgather the solver uses, on `device`; *max_err is the
+ * largest deviation from the expected bytes (0 when the transport works). */
+int mad_comm_selftest(int32_t device, double *max_err);
 /* slab [z_begin, z_end) of this rank for a global nz (even-aligned split) */
 int mad_slab_range(int64_t nz, int32_t nranks, int32_t rank, int32_t align, int64_t *z_begin,
                    int64_t *z_end);

@@ -99,9 +99,16 @@ class Comm {
   void init(const void* uid128, int nranks, int rank, int device) {
     destroy();
     if (nranks <= 1) return;
+    init_rccl(uid128, nranks, rank);
+    (void)device;
+  }
+
+  // an RCCL communicator of any size, one rank included (the transport self-test,
+  // mad_comm_selftest: a single-rank communicator exchanges with itself)
+  void init_rccl(const void* uid128, int nranks, int rank) {
+    destroy();
     ncclUniqueId id;
     std::memcpy(&id, uid128, sizeof(id));
-    (void)device;
     NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
     mode_ = RCCL;
     nranks_ = nranks;
@@ -140,14 +147,17 @@ class Comm {
     if (mode_ == RCCL) {
       const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
       const size_t cnt = (size_t)plane * depth;
+      // neighbour ranks (has_lo / has_hi are false at the global ends; the modulo only
+      // matters for the single-rank self-test, where both neighbours are this rank)
+      const int lo = (rank_ - 1 + nranks_) % nranks_, hi = (rank_ + 1) % nranks_;
       NCCL_CHECK(ncclGroupStart());
       if (has_lo) {
-        NCCL_CHECK(ncclSend(base, cnt, dt, rank_ - 1, comm_, s));
-        NCCL_CHECK(ncclRecv(base - depth * pb, cnt, dt, rank_ - 1, comm_, s));
+        NCCL_CHECK(ncclSend(base, cnt, dt, lo, comm_, s));
+        NCCL_CHECK(ncclRecv(base - depth * pb, cnt, dt, lo, comm_, s));
       }
       if (has_hi) {
-        NCCL_CHECK(ncclSend(base + (size_t)(nz - depth) * pb, cnt, dt, rank_ + 1, comm_, s));
-        NCCL_CHECK(ncclRecv(base + (size_t)nz * pb, cnt, dt, rank_ + 1, comm_, s));
+        NCCL_CHECK(ncclSend(base + (size_t)(nz - depth) * pb, cnt, dt, hi, comm_, s));
+        NCCL_CHECK(ncclRecv(base + (size_t)nz * pb, cnt, dt, hi, comm_, s));
       }
       NCCL_CHECK(ncclGroupEnd());
       return;

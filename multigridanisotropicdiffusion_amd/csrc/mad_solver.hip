@@ -2091,6 +2091,62 @@ int mad_comm_init(mad_ctx* c, const void* uid128) {
   });
 }
 
+int mad_comm_selftest(int32_t device, double* max_err) {
+  if (!max_err) return MAD_ERR_INVALID;
+  return guarded(nullptr, [&] {
+    HIP_CHECK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    char uid[128];
+    Comm::unique_id(uid);
+    Comm comm;
+    comm.init_rccl(uid, 1, 0);
+    // a float slab of NZ planes of P elements with GHOST ghost planes per side; plane z
+    // (ghosts included) holds z + e / P
+    constexpr int NZ = 12, P = 96 * 80;
+    const int NT = NZ + 2 * GHOST;
+    std::vector<float> h((size_t)NT * P);
+    for (int z = 0; z < NT; ++z)
+      for (int e = 0; e < P; ++e) h[(size_t)z * P + e] = (float)(z - GHOST) + (float)e / P;
+    float* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, sizeof(float) * h.size()));
+    HIP_CHECK(hipMemcpy(d, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+    float* base = d + (size_t)GHOST * P;
+    comm.exchange_planes(base, P, NZ, GHOST, 1, 1, sizeof(float), false, s);
+    // allreduce of one fp64 value, allgather of the (single) slab
+    double* v = nullptr;
+    HIP_CHECK(hipMalloc(&v, sizeof(double)));
+    const double one = 1.25;
+    HIP_CHECK(hipMemcpy(v, &one, sizeof one, hipMemcpyHostToDevice));
+    comm.allreduce_sum_f64(v, 1, s);
+    float* g = nullptr;
+    HIP_CHECK(hipMalloc(&g, sizeof(float) * (size_t)NZ * P));
+    comm.allgather_slabs(base, g, P, NZ, sizeof(float), s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<float> o(h.size()), og((size_t)NZ * P);
+    double vr = 0.0;
+    HIP_CHECK(hipMemcpy(o.data(), d, sizeof(float) * o.size(), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(og.data(), g, sizeof(float) * og.size(), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(&vr, v, sizeof vr, hipMemcpyDeviceToHost));
+    // sends and receives between one pair of ranks match in issue order: the lower
+    // ghosts receive the slab's first GHOST planes, the upper ghosts its last GHOST
+    double err = std::fabs(vr - one);
+    for (int z = 0; z < NT; ++z) {
+      const int src = z < GHOST ? GHOST + z : (z >= NZ + GHOST ? z - GHOST : z);
+      for (int e = 0; e < P; ++e)
+        err = std::max(err, (double)std::fabs(o[(size_t)z * P + e] - h[(size_t)src * P + e]));
+    }
+    for (size_t q = 0; q < og.size(); ++q)
+      err = std::max(err, (double)std::fabs(og[q] - h[(size_t)GHOST * P + q]));
+    *max_err = err;
+    comm.destroy();
+    (void)hipFree(d);
+    (void)hipFree(v);
+    (void)hipFree(g);
+    (void)hipStreamDestroy(s);
+  });
+}
+
 int mad_comm_init_local(mad_ctx* c, uint64_t group) {
   if (!c) return MAD_ERR_INVALID;
   return guarded(c, [&] {

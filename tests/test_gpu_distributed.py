@@ -123,3 +123,19 @@ def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel, cycle):
     out = D.run_local(nranks, body, shape, time_step=0.4, gs_kernel=gs_kernel, cycle=cycle)
     np.testing.assert_array_equal(np.concatenate([o[0] for o in out]), ref[0])
     np.testing.assert_array_equal(np.concatenate([o[1] for o in out]), ref[1])
+
+
+def test_rccl_transport_selftest():
+    """The RCCL path on a one-GPU box: a single-rank communicator runs the solver's halo
+    exchange (grouped ncclSend/ncclRecv with this rank as both neighbours), the fp64
+    allreduce and the slab allgather (mad_comm_selftest); every byte lands where the
+    multi-rank exchange would put its neighbour's planes."""
+    import ctypes
+    import os
+    import multigridanisotropicdiffusion_amd as M
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")  # one node: bootstrap on loopback
+    L = M.capi.load()
+    err = ctypes.c_double(-1.0)
+    rc = L.mad_comm_selftest(0, ctypes.byref(err))
+    assert rc == 0, L.mad_last_error(None)
+    assert err.value == 0.0
