@@ -1607,6 +1607,78 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
   }
 }
 
+// 3D coefficient fields, z-marching: a 64 x 4 block of columns walks its planes and keeps
+// the z-derivative components M_xz, M_yz, M_zz of planes k-1, k, k+1 in registers, so the
+// z-neighbour reads of g (one plane away, evicted from L2 by the time a per-plane grid
+// reaches them) come from the previous iterations; in-plane neighbours and the one-sided
+// border formulas read memory as build_coef_k does.  Same arithmetic and order, so the
+// coefficients are bit-identical to build_coef_k's.
+template <typename T, int KIND>
+__global__ void __launch_bounds__(256) build_coef3_k(const double* __restrict__ M, int nx, int ny,
+                                                     int nz, CoefFactors f, T* __restrict__ cf,
+                                                     int rs, int kc) {
+  using L = CoefLayout<3, KIND>;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, nz);
+  if (i >= nx || j >= ny || k0 >= k1) return;
+  const int64_t n = (int64_t)nx * ny * nz, sz = (int64_t)nx * ny;
+  const int64_t col = i + (int64_t)nx * j;
+  const int64_t orow = ((int64_t)nx * j + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1)));
+  const int nn[3] = {nx, ny, nz};
+  const int64_t st[3] = {1, nx, sz};
+  // z-window of M_{d,z}, d = x, y, z (components tcomp(3, d, 2) = 2, 4, 5)
+  const double* Mz[3] = {M + 2 * n, M + 4 * n, M + 5 * n};
+  double zm[3], z0v[3], zp[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    zm[d] = k0 > 0 ? Mz[d][col + (int64_t)(k0 - 1) * sz] : 0.0;
+    z0v[d] = Mz[d][col + (int64_t)k0 * sz];
+    zp[d] = k0 + 1 < nz ? Mz[d][col + (int64_t)(k0 + 1) * sz] : 0.0;
+  }
+  for (int k = k0; k < k1; ++k) {
+    const int64_t p = col + (int64_t)k * sz;
+    const int64_t o = (orow + (int64_t)k * sz) * rs;
+    const int id[3] = {i, j, k};
+    if (KIND == KISO) {
+      cf[o] = (T)(f.fa[0] * M[p]);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) cf[o + d] = (T)(f.fa[d] * M[tcomp(3, d, d) * n + p]);
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      double s = 0.0;
+#pragma unroll
+      for (int d2 = 0; d2 < 3; ++d2) {
+        double dl;
+        if (d2 == 2 && k > 0 && k < nz - 1) {
+          dl = zp[d] - zm[d];  // delta_f's interior formula, from the register window
+        } else {
+          dl = delta_f(M + tcomp(3, d, d2) * n, p, id[d2], nn[d2], st[d2]);
+        }
+        s += dl * f.fg[d2];
+      }
+      cf[o + L::NA + d] = (T)(f.fgo[d] * s);
+    }
+    if (KIND == KFULL) {
+      int e = L::NA + L::NG;
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int d2 = d + 1; d2 < 3; ++d2, ++e)
+          cf[o + e] = (T)(f.fe[d][d2] * M[tcomp(3, d, d2) * n + p]);
+    }
+    // shift the window one plane up
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      zm[d] = z0v[d];
+      z0v[d] = zp[d];
+      zp[d] = k + 2 < nz ? Mz[d][col + (int64_t)(k + 2) * sz] : 0.0;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // deterministic synthetic inputs (bench / smoke), mirrored in tests/synth.py
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {

@@ -1409,11 +1409,28 @@ class Solver final : public SolverBase {
         dst = full_cf;
       }
       dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
-      dispatch(dim, c_->kind, [&](auto D, auto K) {
-        hipLaunchKernelGGL((build_coef_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
-                           (int)G.n[0], (int)G.n[1], (int)G.n[2],
-                           coef_factors(G.h, c_->d.time_step), dst, L.g.rs);
-      });
+      if (dim == 3) {
+        // z-marching (build_coef3_k): chunks of planes sized for ~4096 blocks of 64 x 4
+        const int bx = ((int)G.n[0] + 63) / 64, by = ((int)G.n[1] + 3) / 4;
+        const int nzg = (int)G.n[2];
+        int chunks = std::max(1, std::min(nzg, (4096 + bx * by - 1) / (bx * by)));
+        const int kc = (nzg + chunks - 1) / chunks;
+        chunks = (nzg + kc - 1) / kc;
+        auto go = [&](auto K) {
+          hipLaunchKernelGGL((build_coef3_k<T, decltype(K)::value>), dim3(bx, by, chunks), BLK, 0,
+                             c_->stream, fine, (int)G.n[0], (int)G.n[1], nzg,
+                             coef_factors(G.h, c_->d.time_step), dst, L.g.rs, kc);
+        };
+        if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
+        else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
+        else go(std::integral_constant<int, KISO>{});
+      } else {
+        dispatch(dim, c_->kind, [&](auto D, auto K) {
+          hipLaunchKernelGGL((build_coef_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
+                             (int)G.n[0], (int)G.n[1], (int)G.n[2],
+                             coef_factors(G.h, c_->d.time_step), dst, L.g.rs);
+        });
+      }
       HIP_CHECK(hipGetLastError());
       if (slab) {
         // owned planes plus up to GHOST neighbour planes on each side (whole plane blocks)
