@@ -1136,6 +1136,120 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
   }
 }
 
+// wj3_k: one weighted-Jacobi sweep (itkMultigridWeightedJacobiSmoother.hxx:67-98),
+// z-marching like resid3_k: u planes staged once in a 4-plane LDS ring with the x/y
+// mirror images, the record of the next plane prefetched, uo written out of place.
+// Same point update as wj_k: (b + S) * (omega / D) + (1 - omega) u.
+template <typename T, int KIND, int TX, int TY, bool BREC = false>
+__global__ void __launch_bounds__(TX * TY) wj3_k(const T* __restrict__ u, T* __restrict__ uo,
+                                                 const T* __restrict__ b, const T* __restrict__ cf,
+                                                 Geo g, Rat<T> rat, T omega, int zc, int ntx) {
+  constexpr int NT = TX * TY;
+  constexpr int RX = TX + 2, RY = TY + 2, PL = RX * RY;
+  constexpr int UPT = (PL + NT - 1) / NT;
+  constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr int RS = NCF + (BREC ? 1 : 0);
+  constexpr uint32_t TS = sizeof(T);
+  __shared__ T ring[4 * PL];
+  const int tiles_per_plane = ntx * ((g.ny + TY - 1) / TY);
+  const int chunk = blockIdx.x / tiles_per_plane;
+  const int tile = blockIdx.x - chunk * tiles_per_plane;
+  const int tyi = tile / ntx, txi = tile - (tile / ntx) * ntx;
+  const int x0 = txi * TX, y0 = tyi * TY;
+  const int tid = threadIdx.x;
+  const int tx = tid % TX, ty = tid / TX;
+  const int nx = g.nx, ny = g.ny, sy = (int)g.sy, hx0 = g.hx0;
+  const int64_t sz = g.sz;
+  const int z0 = chunk * zc, z1 = min(z0 + zc, g.nz);
+  const int zlo = g.zlo_ghost ? -1 : 0, zhi = g.zhi_ghost ? g.nz + 1 : g.nz;
+  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
+  int u_dst[UPT];
+  uint32_t u_src[UPT];
+#pragma unroll
+  for (int e = 0; e < UPT; ++e) {
+    const int q = tid + e * NT;
+    const int lj = q / RX, li = q - (q / RX) * RX;
+    u_dst[e] = q < PL ? q : -1;
+    u_src[e] = (uint32_t)(mirror(y0 - 1 + lj, ny) * sy + mirror(x0 - 1 + li, nx)) * TS;
+  }
+  const int i = x0 + tx, j = y0 + ty;
+  const bool ok = i < nx && j < ny;
+  const uint32_t rec_off = ok ? (uint32_t)(ty * sy + (tx & 1) * hx0 + (tx >> 1)) * (TS * RS) : 0u;
+  const uint32_t pt_off = ok ? (uint32_t)(ty * sy + tx) * TS : 0u;
+  const int64_t rbase = (int64_t)y0 * sy + (x0 >> 1), pbase = (int64_t)y0 * sy + x0;
+  const int il = (ty + 1) * RX + (tx + 1);
+  constexpr int oyp = RX, oym = -RX;
+
+  T up[UPT];
+  T raw[RS];
+  T bv = T(0);
+  auto load_plane = [&](int m) {
+    m = min(max(m, zlo), zhi - 1);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src[e], 0u);
+  };
+  auto put_plane = [&](int m) {
+    T* P = ring + (m & 3) * PL;
+#pragma unroll
+    for (int e = 0; e < UPT; ++e)
+      if (e < UPT - 1 || u_dst[e] >= 0) P[u_dst[e]] = up[e];
+  };
+  auto load_pt = [&](int m) {
+    m = min(max(m, 0), g.nz - 1);
+    buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + rbase) * RS), rec_off, raw);
+    if constexpr (!BREC) bv = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + pbase), pt_off, 0u);
+  };
+
+  if (z0 - 1 >= zlo) {
+    load_plane(z0 - 1);
+    put_plane(z0 - 1);
+  }
+  load_plane(z0);
+  put_plane(z0);
+  load_plane(z0 + 1);
+  load_pt(z0);
+  for (int m = z0; m < z1; ++m) {
+    if (m + 1 < zhi) put_plane(m + 1);
+    load_plane(m + 2);
+    __syncthreads();
+    const int zm = (m == 0 && !g.zlo_ghost) ? m + 1 : m - 1;
+    const int zp = (m == g.nz - 1 && !g.zhi_ghost) ? m - 1 : m + 1;
+    const T* P0 = ring + (m & 3) * PL + il;
+    const T* Pm = ring + (zm & 3) * PL + il;
+    const T* Pp = ring + (zp & 3) * PL + il;
+    T nb[18];
+    nb[0] = P0[1];
+    nb[1] = P0[-1];
+    nb[2] = P0[oyp];
+    nb[3] = P0[oym];
+    nb[4] = Pp[0];
+    nb[5] = Pm[0];
+    if (KIND == KFULL) {
+      nb[6] = P0[1 + oyp];
+      nb[7] = P0[1 + oym];
+      nb[8] = P0[-1 + oyp];
+      nb[9] = P0[-1 + oym];
+      nb[10] = Pp[1];
+      nb[11] = Pm[1];
+      nb[12] = Pp[-1];
+      nb[13] = Pm[-1];
+      nb[14] = Pp[oyp];
+      nb[15] = Pm[oyp];
+      nb[16] = Pp[oym];
+      nb[17] = Pm[oym];
+    }
+    Coefs<T> q;
+    coefs_from_raw<T, 3, KIND>(raw, rat, q);
+    T D, S;
+    stencil_combine<T, 3, KIND>(q, nb, D, S);
+    T v = ((BREC ? raw[NCF] : bv) + S) * (omega / D);
+    v += (T(1) - omega) * P0[0];
+    load_pt(m + 1);
+    if (ok) buf_store<T>(v, buf_rsrc(uo + (int64_t)m * sz + pbase), pt_off);
+  }
+}
+
 // sum of squares of a contiguous array, grid-stride, fp64 partials per block
 template <typename T>
 __global__ void __launch_bounds__(256) sumsq_k(const T* __restrict__ x, int64_t n,

@@ -638,7 +638,11 @@ class Solver final : public SolverBase {
     const int dim = c_->dim, kind = c_->kind;
     char buf[160];
     if (c_->d.smoother == MAD_WEIGHTED_JACOBI) {
-      std::snprintf(buf, sizeof buf, "wj_k<%s, %d, %d>", tn, dim, kind);
+      const LevelData<T>& L = lv_[l];
+      if (dim == 3 && L.g.nx >= 16 && L.g.ny >= 16)
+        std::snprintf(buf, sizeof buf, "wj3_k<%s, %d, 64, 16%s>", tn, kind, L.brec ? ", true" : "");
+      else
+        std::snprintf(buf, sizeof buf, "wj_k<%s, %d, %d>", tn, dim, kind);
     } else if (c_->d.smoother == MAD_GAUSS_SEIDEL_LEX) {
       std::snprintf(buf, sizeof buf, "gs_lex_plane_k<%s, %d, %d>", tn, dim, kind);
     } else if (!use_fused(l)) {
@@ -762,19 +766,52 @@ class Solver final : public SolverBase {
     return 0.f;
   }
 
+  // weighted Jacobi: ghost planes / record b before the sweep, then the sweep kernel --
+  // z-marching wj3_k on 3D levels of at least 16 x 16 (LDS-staged u planes), wj_k else
+  void prep_wj(int l) {
+    LevelData<T>& L = lv_[l];
+    halo(l, L.x);
+    if (L.brec) sync_brec(l);
+  }
+  void launch_wj(int l) {
+    LevelData<T>& L = lv_[l];
+    const T omega = (T)c_->d.omega;
+    if (c_->dim == 3 && L.g.nx >= 16 && L.g.ny >= 16) {
+      constexpr int TX = 64, TY = 16;
+      const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
+      int chunks = std::max(1, std::min((1024 + ntx * nty - 1) / (ntx * nty), L.g.nz / 8));
+      const int zc = (L.g.nz + chunks - 1) / chunks;
+      chunks = (L.g.nz + zc - 1) / zc;
+      const unsigned nb = (unsigned)(ntx * nty * chunks);
+      auto go = [&](auto K) {
+        constexpr int KD = decltype(K)::value;
+        if (L.brec)
+          hipLaunchKernelGGL((wj3_k<T, KD, TX, TY, true>), dim3(nb), dim3(TX * TY), 0, c_->stream,
+                             L.x, L.t, L.b, L.cf, L.g, L.rat, omega, zc, ntx);
+        else
+          hipLaunchKernelGGL((wj3_k<T, KD, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, L.x,
+                             L.t, L.b, L.cf, L.g, L.rat, omega, zc, ntx);
+      };
+      if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
+      else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
+      else go(std::integral_constant<int, KISO>{});
+    } else {
+      dispatch(c_->dim, c_->kind, [&](auto D, auto K) {
+        hipLaunchKernelGGL((wj_k<T, D.value, K.value>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK), BLK,
+                           0, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat, omega);
+      });
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+
   void smooth(int l, unsigned n) override {
     LevelData<T>& L = lv_[l];
     const int dim = c_->dim;
     const int sm = c_->d.smoother;
     for (unsigned s = 0; s < n; ++s) {
       if (sm == MAD_WEIGHTED_JACOBI) {
-        halo(l, L.x);
-        dispatch(dim, c_->kind, [&](auto D, auto K) {
-          hipLaunchKernelGGL((wj_k<T, D.value, K.value>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK),
-                             BLK, 0, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                             (T)c_->d.omega);
-        });
-        HIP_CHECK(hipGetLastError());
+        prep_wj(l);
+        launch_wj(l);
         std::swap(L.x, L.t);
         std::swap(L.alloc[0], L.alloc[3]);
         x_changed(l);
@@ -1221,13 +1258,9 @@ class Solver final : public SolverBase {
     unsigned q = 0;
     for (unsigned s = 0; s < n; ++s) {
       if (sm == MAD_WEIGHTED_JACOBI) {
-        halo(l, L.x);
+        prep_wj(l);
         HIP_CHECK(hipEventRecord(ev[2 * q], c_->stream));
-        dispatch(c_->dim, c_->kind, [&](auto D, auto K) {
-          hipLaunchKernelGGL((wj_k<T, D.value, K.value>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK),
-                             BLK, 0, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                             (T)c_->d.omega);
-        });
+        launch_wj(l);
         HIP_CHECK(hipEventRecord(ev[2 * q + 1], c_->stream));
         ++q;
         std::swap(L.x, L.t);
