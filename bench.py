@@ -177,10 +177,10 @@ def main():
         if dist is not None:
             dist.barrier()
         return
-    # roofline of the dominant kernel: the fused GS sweep processes the whole slab per
-    # launch; the per-colour variant one colour class (1/4 of the slab) per launch
-    ncolors = 4 if (a.smoother == "gs" and a.gs_kernel == 1) else 1
-    units_per_launch = float(shape[0] * shape[1] * shape[2]) / ncolors
+    # roofline of the dominant kernel: voxel updates per launch from the launch count the
+    # library reports (the fused GS / WJ sweep: the whole slab per launch; per-colour GS
+    # passes: one colour class per launch)
+    units_per_launch = float(shape[0] * shape[1] * shape[2]) * a.steps / max(1, launches)
     achieved = BYTES_PER_VOXEL_SMOOTH * units_per_launch / (kern_ms * 1e-3) / 1e9
     tag = f"{a.smoother}_{S}"
     kname = s.smooth_kernel_name(0)  # as rocprofv3 prints it (profiles/ are matched on it)

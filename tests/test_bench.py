@@ -1,0 +1,48 @@
+"""bench.py's output contract: the CPU baseline leg (runs here) and one short bench run on
+the GPU (a reduced volume; the JSON line's keys and their consistency)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_cpu_baseline_leg_reports_the_oracle():
+    sys.path.insert(0, ROOT)
+    import bench
+    cb = bench.cpu_baseline(0.05)
+    assert cb["value"] > 0 and cb["unit"] == "Mvoxel-smooths/s"
+    assert cb["cores"] == 1 and cb["kind"] == "port" and "128^3" in cb["sample"]
+    par = cb["parallel"]
+    assert par["value"] > 0 and par["cores"] >= 1 and par["kind"] == "port"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--smoother", "wj"], ["--gs-kernel", "1"]])
+def test_bench_json_line(extra):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--size", "256", "--steps", "4",
+           "--warmup", "1", "--vcycles", "2", "--no-cpu-baseline"] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["dtype"] == "f32"
+    assert d["value"] > 0 and d["vcycles_per_s"] > 0
+    # value = voxels x steps / wall time
+    assert abs(d["value"] - 256 ** 3 * 4 / (d["ms_per_step"] * 4e-3) / 1e6) <= 0.01 * d["value"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and r["unit"] == "GB/s"
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    # per-colour passes: four launches per sweep, each a quarter of the voxels
+    nl = 4 if extra == ["--gs-kernel", "1"] else 1
+    assert r["launches"] == 4 * nl
+    assert r["algorithmic_bytes_per_launch"] == 36.0 * 256 ** 3 / nl
+    assert 0 < r["kernel_ms_min"] <= r["kernel_ms_median"]
