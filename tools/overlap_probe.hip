@@ -19,10 +19,15 @@
     }                                                                               \
   } while (0)
 
+// device timestamps (constant wall clock) independent of event packets: ts[0] busy start
+// (block 0), ts[1] max copy end
+__device__ unsigned long long g_ts[2];
+
 // busy kernel: each workgroup streams its own slice `iters` times; signals after iter 1
 __global__ void __launch_bounds__(1024) busy(const float4* __restrict__ a, float* __restrict__ out,
                                              long per_wg4, int iters, unsigned* sig, int early) {
   extern __shared__ float4 lds[];
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_ts[0] = wall_clock64();
   if (early && sig && threadIdx.x == 0)
     __hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   float acc = 0.f;
@@ -56,6 +61,8 @@ __global__ void tiny(float* o) {
 
 __global__ void __launch_bounds__(256) copyk(const float4* __restrict__ s, float4* __restrict__ d, long n4) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) d[i] = s[i];
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&g_ts[1], (unsigned long long)wall_clock64());
 }
 
 int main() {
@@ -70,6 +77,13 @@ int main() {
   CK(hipMalloc(&o, 4096));
   CK(hipMemset(a, 0, per_wg * 256));
   CK(hipExtMallocWithFlags((void**)&sig, 8, hipMallocSignalMemory));
+  // mode 3: the counter in coherent host memory, polled by the host thread
+  unsigned* hsig = nullptr;
+  unsigned* hsig_d = nullptr;
+  CK(hipHostMalloc((void**)&hsig, 8, hipHostMallocCoherent | hipHostMallocMapped));
+  CK(hipHostGetDevicePointer((void**)&hsig_d, hsig, 0));
+  hsig[0] = 0;
+  unsigned htarget = 0;
   unsigned zero = 0;
   CK(hipMemcpy(sig, &zero, 4, hipMemcpyHostToDevice));
   int can = 0;
@@ -84,12 +98,28 @@ int main() {
   CK(hipEventCreate(&e1));
   CK(hipEventCreate(&e2));
   unsigned target = 0;
-  for (int mode = 0; mode < 3; ++mode)
+  for (int mode = 0; mode < 7; ++mode)
     for (int rep = 0; rep < 3; ++rep) {
       // mode 0: signal after the first quarter; 1: signal at kernel start; 2: event after a tiny
-      // kernel that precedes the big one on stream A (the boundary-launch pattern)
+      // kernel that precedes the big one on stream A (the boundary-launch pattern); 3: signal
+      // at kernel start into host memory, the host thread polls it and then launches the copy
       CK(hipEventRecord(e0, A));
-      if (mode == 2) {
+      // 4: as 3 with 248 workgroups (one CU per XCD left free); 5: as 1 with 248 workgroups
+      // 6: as 1 with a 1024-workgroup copy (is the delay the copy's own run under the big
+      // kernel's HBM load rather than the wake-up?)
+      if (mode == 5) {
+        hipLaunchKernelGGL(busy, dim3(248), dim3(1024), 93 * 1024, A, a, o, per_wg / 16, iters + 3, sig, 1);
+        target += 248u;
+        CK(hipStreamWaitEvent(B, e0, 0));
+        CK(hipStreamWaitValue32(B, sig, target, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      } else if (mode == 3 || mode == 4) {
+        const unsigned nb = mode == 3 ? 256u : 248u;
+        hipLaunchKernelGGL(busy, dim3(nb), dim3(1024), 93 * 1024, A, a, o, per_wg / 16, iters + 3, hsig_d,
+                           1);
+        htarget += nb;
+        while (__atomic_load_n(hsig, __ATOMIC_ACQUIRE) < htarget) {
+        }
+      } else if (mode == 2) {
         hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, A, o);
         CK(hipEventRecord(e1, A));
         CK(hipStreamWaitEvent(B, e1, 0));
@@ -97,12 +127,12 @@ int main() {
                            (unsigned*)nullptr, 0);
       } else {
         hipLaunchKernelGGL(busy, dim3(256), dim3(1024), 93 * 1024, A, a, o, per_wg / 16, iters + 3, sig,
-                           mode);
+                           mode == 6 ? 1 : mode);
         target += 256u;
         CK(hipStreamWaitEvent(B, e0, 0));
         CK(hipStreamWaitValue32(B, sig, target, hipStreamWaitValueGte, 0xFFFFFFFFu));
       }
-      hipLaunchKernelGGL(copyk, dim3(64), dim3(256), 0, B, s, d, (8 << 20) / 16);
+      hipLaunchKernelGGL(copyk, dim3(mode == 6 ? 1024 : 64), dim3(256), 0, B, s, d, (8 << 20) / 16);
       CK(hipEventRecord(e2, B));
       hipEvent_t e3;
       CK(hipEventCreate(&e3));
@@ -112,8 +142,14 @@ int main() {
       CK(hipEventElapsedTime(&big, e0, e3));
       CK(hipEventElapsedTime(&cp, e0, e2));
       CK(hipEventDestroy(e3));
-      std::printf("{\"mode\": %d, \"rep\": %d, \"big_kernel_ms\": %.3f, \"copy_done_ms_after_start\": %.3f}\n",
-                  mode, rep, big, cp);
+      unsigned long long ts[2];
+      CK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_ts), sizeof(ts)));
+      int khz = 0;
+      CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
+      const double dev_ms = (double)((long long)(ts[1] - ts[0])) / (double)khz;
+      std::printf("{\"mode\": %d, \"rep\": %d, \"big_kernel_ms\": %.3f, \"copy_done_ms_after_start\": %.3f, "
+                  "\"copy_end_after_busy_start_ms_device_clock\": %.3f}\n",
+                  mode, rep, big, cp, dev_ms);
     }
   // copy kernel alone
   CK(hipEventRecord(e0, B));
