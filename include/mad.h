@@ -183,6 +183,11 @@ int mad_residual(mad_ctx *ctx, int32_t level, double *norm_out);
 int mad_norm(mad_ctx *ctx, int32_t level, int32_t which, double *norm_out);
 /* IGO.hxx:175-304 Restriction: b[level+1] <- R r[level]. */
 int mad_restrict(mad_ctx *ctx, int32_t level);
+/* MAD.hxx:389,413 the V-cycle descent b[level+1] <- R (b[level] - A x[level]) in one pass
+ * (r[level] is not written) where the level is held whole by this rank (3D, >= 16 x 16);
+ * elsewhere residual + restriction.  *fused (optional) = 1 if the one-pass kernel ran.
+ * Bit-identical to mad_residual + mad_restrict. */
+int mad_residual_restrict(mad_ctx *ctx, int32_t level, int32_t *fused);
 /* IGO.hxx:45-172 Interpolation: x[level] <- P x[level+1]. */
 int mad_interpolate(mad_ctx *ctx, int32_t level);
 /* IGO Interpolation + correction add (MAD.hxx:422-435): x[level] += P x[level+1]. */

@@ -34,6 +34,7 @@ EXPORTS = (
     "mad_run_device", "mad_get_step_stats", "mad_num_levels", "mad_plan_level",
     "mad_level_info", "mad_upload",
     "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
+    "mad_residual_restrict",
     "mad_interpolate", "mad_prolongate_add", "mad_coarse_solve", "mad_vcycle", "mad_fmg",
     "mad_synchronize", "mad_bench_smooth", "mad_bench_launch_times", "mad_smooth_kernel_name", "mad_bench_vcycle", "mad_bench_synth_tensor",
     "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_comm_init_local",
@@ -187,6 +188,7 @@ def load():
         "mad_residual": ([vp, i32, dp], i32),
         "mad_norm": ([vp, i32, i32, dp], i32),
         "mad_restrict": ([vp, i32], i32),
+        "mad_residual_restrict": ([vp, i32, ctypes.POINTER(i32)], i32),
         "mad_interpolate": ([vp, i32], i32),
         "mad_prolongate_add": ([vp, i32], i32),
         "mad_coarse_solve": ([vp], i32),

@@ -1482,6 +1482,185 @@ __global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fin
   }
 }
 
+// resid_restrict3_k: the coarse right-hand side b_c = R (b - A u) of one V-cycle descent
+// (MAD.hxx:389,413) in one pass, without storing the fine residual.  Coarse tile CX x CY
+// and coarse planes [K0, K1) as restrict3_k; each fine plane the chunk's taps need is
+// residualised on restrict3_k's fine tile (2CX+2 x 2CY+2, fine indices clamped into
+// the grid) from a 4-slot LDS ring of u planes over that tile + 1 (x/y mirror images
+// in the ring, as resid3_k), the residuals go to an LDS tile, and restrict3_k's x-y
+// taps, z window and emission follow.  Residual arithmetic = resid3_k's, restriction
+// arithmetic = restrict3_k's, so b_c is bit-identical to residual + restriction.
+// One rank (no ghost planes), nx, ny >= 3, nz >= 2.
+template <typename T, int KIND, int CX, int CY, int NT, bool BREC = false>
+__global__ void __launch_bounds__(NT) resid_restrict3_k(
+    const T* __restrict__ u, const T* __restrict__ b, const T* __restrict__ cf, Geo gf, Rat<T> rat,
+    T* __restrict__ coarse, Geo gc, int cx, int cy, int cz, int kc, int ntx) {
+  static_assert(CX * CY <= NT, "one coarse point per thread");
+  constexpr int FX = 2 * CX + 2, FY = 2 * CY + 2, FP = FX * FY;  // residual tile
+  constexpr int UX = FX + 2, UY = FY + 2, UP = UX * UY;          // u region (tile + 1)
+  constexpr int UPT = (UP + NT - 1) / NT;
+  constexpr int RPT = (FP + NT - 1) / NT;
+  constexpr int NCF = CoefLayout<3, KIND>::N;
+  constexpr int RS = NCF + (BREC ? 1 : 0);
+  constexpr uint32_t TS = sizeof(T);
+  __shared__ T ring[4 * UP];
+  __shared__ T rt[FP];
+  const int tiles = ntx * ((gc.ny + CY - 1) / CY);
+  const int chunk = blockIdx.x / tiles;
+  const int t = blockIdx.x - chunk * tiles;
+  const int tyi = t / ntx, txi = t - (t / ntx) * ntx;
+  const int I0 = txi * CX, J0 = tyi * CY;
+  const int tid = threadIdx.x;
+  const int nx = gf.nx, ny = gf.ny, nz = gf.nz, sy = (int)gf.sy, hx0 = gf.hx0;
+  const int64_t sz = gf.sz;
+  const int fx0 = 2 * I0 - 1, fy0 = 2 * J0 - 1;  // residual tile origin (fine indices)
+  const int ux0 = fx0 - 1, uy0 = fy0 - 1;        // u region origin
+  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
+  // coarse point of this thread (threads < CX * CY)
+  const bool cthr = tid < CX * CY;
+  const int I = I0 + tid % CX, J = J0 + (tid / CX) % CY;
+  const bool ok = cthr && I < gc.nx && J < gc.ny;
+  int ix[4], iy[4];
+  T wx[4], wy[4];
+  rtaps4<T>(min(I, gc.nx - 1), gc.nx, cx, ix, wx);
+  rtaps4<T>(min(J, gc.ny - 1), gc.ny, cy, iy, wy);
+  // u region elements: LDS index and mirrored in-plane source offset
+  int u_dst[UPT];
+  uint32_t u_src[UPT];
+#pragma unroll
+  for (int e = 0; e < UPT; ++e) {
+    const int q = tid + e * NT;
+    const int lj = min(q, UP - 1) / UX, li = min(q, UP - 1) - (min(q, UP - 1) / UX) * UX;
+    u_dst[e] = q < UP ? q : -1;
+    u_src[e] = (uint32_t)(mirror(uy0 + lj, ny) * sy + mirror(ux0 + li, nx)) * TS;
+  }
+  // residual tile elements: the clamped fine point, its ring index, record / b offsets
+  int r_il[RPT];
+  uint32_t r_rec[RPT], r_pt[RPT];
+#pragma unroll
+  for (int e = 0; e < RPT; ++e) {
+    const int q = min(tid + e * NT, FP - 1);
+    const int ry = q / FX, rx = q - (q / FX) * FX;
+    const int xf = min(max(fx0 + rx, 0), nx - 1), yf = min(max(fy0 + ry, 0), ny - 1);
+    r_il[e] = (yf - uy0) * UX + (xf - ux0);
+    r_rec[e] = (uint32_t)(yf * sy + (xf & 1) * hx0 + (xf >> 1)) * (TS * RS);
+    r_pt[e] = (uint32_t)(yf * sy + xf) * TS;
+  }
+  const int K0 = chunk * kc, K1 = min(K0 + kc, gc.nz);
+  int iz[4];
+  T wz[4];
+  rtaps4<T>(K0, gc.nz, cz, iz, wz);
+  const int f_lo = iz[0];
+  rtaps4<T>(K1 - 1, gc.nz, cz, iz, wz);
+  const int f_hi = max(max(iz[0], iz[1]), max(iz[2], iz[3]));
+
+  T up[UPT];
+  T raw[RPT][RS];
+  T bv[RPT];
+  auto load_plane = [&](int m) {
+    m = min(max(m, 0), nz - 1);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src[e], 0u);
+  };
+  auto put_plane = [&](int m) {
+    T* P = ring + (m & 3) * UP;
+#pragma unroll
+    for (int e = 0; e < UPT; ++e)
+      if (u_dst[e] >= 0) P[u_dst[e]] = up[e];
+  };
+  // waves whose elements all lie past the tile skip that element's loads and arithmetic
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+  auto wave_in = [&](int e) { return wbase + e * NT < FP; };
+  auto load_pts = [&](int m) {
+    m = min(max(m, 0), nz - 1);
+    const __amdgpu_buffer_rsrc_t rr = buf_rsrc(cf + (int64_t)m * sz * RS);
+    const __amdgpu_buffer_rsrc_t rb = buf_rsrc(b + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < RPT; ++e) {
+      if (e > 0 && !wave_in(e)) continue;
+      buf_load_rec<T, RS>(rr, r_rec[e], raw[e]);
+      if constexpr (!BREC) bv[e] = buf_load<T>(rb, r_pt[e], 0u);
+    }
+  };
+
+  if (f_lo - 1 >= 0) {
+    load_plane(f_lo - 1);
+    put_plane(f_lo - 1);
+  }
+  load_plane(f_lo);
+  put_plane(f_lo);
+  load_plane(f_lo + 1);
+  load_pts(f_lo);
+  T win[4];
+  int K = K0;
+  rtaps4<T>(K, gc.nz, cz, iz, wz);
+  for (int f = f_lo; f <= f_hi; ++f) {
+    if (f + 1 < nz) put_plane(f + 1);
+    load_plane(f + 2);
+    __syncthreads();  // ring planes f-1..f+1 staged; last plane's restriction reads of rt done
+    const int zm = f == 0 ? f + 1 : f - 1;
+    const int zp = f == nz - 1 ? f - 1 : f + 1;
+#pragma unroll
+    for (int e = 0; e < RPT; ++e) {
+      if (e > 0 && !wave_in(e)) continue;
+      const T* P0 = ring + (f & 3) * UP + r_il[e];
+      const T* Pm = ring + (zm & 3) * UP + r_il[e];
+      const T* Pp = ring + (zp & 3) * UP + r_il[e];
+      T nb[18];
+      nb[0] = P0[1];
+      nb[1] = P0[-1];
+      nb[2] = P0[UX];
+      nb[3] = P0[-UX];
+      nb[4] = Pp[0];
+      nb[5] = Pm[0];
+      if (KIND == KFULL) {
+        nb[6] = P0[1 + UX];
+        nb[7] = P0[1 - UX];
+        nb[8] = P0[-1 + UX];
+        nb[9] = P0[-1 - UX];
+        nb[10] = Pp[1];
+        nb[11] = Pm[1];
+        nb[12] = Pp[-1];
+        nb[13] = Pm[-1];
+        nb[14] = Pp[UX];
+        nb[15] = Pm[UX];
+        nb[16] = Pp[-UX];
+        nb[17] = Pm[-UX];
+      }
+      Coefs<T> q;
+      coefs_from_raw<T, 3, KIND>(raw[e], rat, q);
+      T D, S;
+      stencil_combine<T, 3, KIND>(q, nb, D, S);
+      const T rv = resid_value(BREC ? raw[e][NCF] : bv[e], D, P0[0], S);
+      if (tid + e * NT < FP) rt[tid + e * NT] = rv;
+    }
+    if (f < f_hi) load_pts(f + 1);
+    __syncthreads();  // residual tile of plane f complete
+    {
+#pragma clang fp contract(off)  // restrict3_k's explicit-fma order
+      T vz = T(0);
+#pragma unroll
+      for (int bq = 0; bq < 4; ++bq) {
+        const T* row = rt + (iy[bq] - fy0) * FX - fx0;
+        T vy = T(0);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) vy = fma(wx[a], row[ix[a]], vy);
+        vz = fma(wy[bq], vy, vz);
+      }
+      win[f & 3] = vz;
+      while (K < K1 && max(max(iz[0], iz[1]), max(iz[2], iz[3])) == f) {
+        T v = T(0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v = fma(wz[c], win[iz[c] & 3], v);
+        if (ok) coarse[I + gc.sy * J + gc.sz * (int64_t)K] = v;
+        ++K;
+        if (K < K1) rtaps4<T>(K, gc.nz, cz, iz, wz);
+      }
+    }
+  }
+}
+
 // interp3_k: fine tile TX x TY (one thread per fine point), fine planes [k0, k1),
 // marched in groups of G planes: the coarse planes a group's taps span go into an
 // 8-slot LDS ring (only the ones not already there), and the fine values of the NEXT

@@ -221,6 +221,7 @@ struct SolverBase {
   virtual double residual(int l, bool want_norm) = 0;
   virtual double norm(int l, int which) = 0;
   virtual void restrict_(int l) = 0;
+  virtual bool residual_restrict(int l) = 0;  // fused b[l+1] <- R (b - A x); false: not applicable
   virtual void interpolate(int l, bool add) = 0;
   virtual void coarse_solve() = 0;
   virtual void vcycle() = 0;
@@ -915,6 +916,60 @@ class Solver final : public SolverBase {
   // b[l+1] <- R r[l]   (IGO.hxx:175-304)
   void restrict_(int l) override { restrict_arr(l, lv_[l].r, lv_[l + 1].b); }
 
+  // b[l+1] <- R (b[l] - A x[l]) in one pass (resid_restrict3_k, bit-identical to the
+  // residual + restriction pair; r[l] is not written).  3D levels held whole by this
+  // rank (one GPU, or the replicated coarse levels); false: not applicable, the caller
+  // runs residual + restriction.  MAD_FUSED_RR=0 turns it off (A/B runs).
+  bool residual_restrict(int l) override { return resid_restrict(l); }
+  bool resid_restrict(int l) {
+    static const bool on = [] {
+      const char* e = std::getenv("MAD_FUSED_RR");
+      return !(e && e[0] == '0');
+    }();
+    LevelData<T>& F = lv_[l];
+    LevelData<T>& C = lv_[l + 1];
+    if (!on || c_->dim != 3 || c_->geom[l].distributed || c_->geom[l + 1].distributed ||
+        F.g.zlo_ghost || F.g.zhi_ghost || F.g.nx < 16 || F.g.ny < 16 || F.g.nz < 2)
+      return false;
+    sync_brec(l);
+    C.b_halo_ok = C.brec_ok = false;
+    static const int tile = [] {
+      const char* e = std::getenv("MAD_RR_TILE");  // tuning runs only: 0 32x8, 1 32x16 coarse
+      return e ? std::atoi(e) : 0;
+    }();
+    static const int target = [] {
+      const char* e = std::getenv("MAD_RR_BLOCKS");  // tuning runs only
+      return e ? std::max(1, std::atoi(e)) : 512;
+    }();
+    auto run = [&](auto CXc, auto CYc) {
+      constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = 1024;
+      const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
+      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / 4));
+      const int kc = (C.g.nz + chunks - 1) / chunks;
+      chunks = (C.g.nz + kc - 1) / kc;
+      const dim3 grid((unsigned)(ntx * nty * chunks)), block(NT);
+      auto go = [&](auto K) {
+        constexpr int KD = decltype(K)::value;
+        if (F.brec)
+          hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT, true>), grid, block, 0, c_->stream,
+                             F.x, F.b, F.cf, F.g, F.rat, C.b, C.g, C.cent[0], C.cent[1], C.cent[2], kc,
+                             ntx);
+        else
+          hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT>), grid, block, 0, c_->stream, F.x,
+                             F.b, F.cf, F.g, F.rat, C.b, C.g, C.cent[0], C.cent[1], C.cent[2], kc, ntx);
+      };
+      if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
+      else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
+      else go(std::integral_constant<int, KISO>{});
+    };
+    if (tile == 1)
+      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 16>{});
+    else
+      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{});
+    HIP_CHECK(hipGetLastError());
+    return true;
+  }
+
   void restrict_arr(int l, T* fine, T* coarse) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
@@ -994,8 +1049,10 @@ class Solver final : public SolverBase {
     } else {
       smooth(l, nu);  // MAD.hxx:384-411
     }
-    residual(l, false);  // MAD.hxx:389 (after the last pre-smoothing sweep)
-    restrict_down(l);    // MAD.hxx:413
+    if (!resid_restrict(l)) {
+      residual(l, false);  // MAD.hxx:389 (after the last pre-smoothing sweep)
+      restrict_down(l);    // MAD.hxx:413
+    }
     fill(l + 1, MAD_X, 0.0);  // MAD.hxx:415-416
     vcycle_rec(l + 1);        // MAD.hxx:418-420
     interpolate_up(l, true);  // MAD.hxx:422-435
@@ -2057,6 +2114,16 @@ int mad_norm(mad_ctx* c, int32_t level, int32_t which, double* norm_out) {
 int mad_restrict(mad_ctx* c, int32_t level) {
   KERNEL_ENTRY(REQUIRE(level >= 0 && level < c->nlev - 1, MAD_ERR_INVALID, "bad level");
                c->solver->restrict_(level));
+}
+
+int mad_residual_restrict(mad_ctx* c, int32_t level, int32_t* fused) {
+  KERNEL_ENTRY(REQUIRE(level >= 0 && level < c->nlev - 1, MAD_ERR_INVALID, "bad level");
+               const bool f = c->solver->residual_restrict(level);
+               if (!f) {
+                 c->solver->residual(level, false);
+                 c->solver->restrict_(level);
+               }
+               if (fused) *fused = f ? 1 : 0);
 }
 
 int mad_interpolate(mad_ctx* c, int32_t level) {

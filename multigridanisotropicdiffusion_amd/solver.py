@@ -178,6 +178,12 @@ class Solver:
     def restrict(self, level):
         self._check(self._L.mad_restrict(self._ctx, level))
 
+    def residual_restrict(self, level):
+        """b[level+1] <- R (b - A x) in one pass where possible; returns True if fused."""
+        f = ctypes.c_int32()
+        self._check(self._L.mad_residual_restrict(self._ctx, level, ctypes.byref(f)))
+        return bool(f.value)
+
     def interpolate(self, level):
         self._check(self._L.mad_interpolate(self._ctx, level))
 

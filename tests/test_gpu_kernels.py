@@ -227,3 +227,36 @@ def test_transfers_random_every_level(name, prec, oracle_mod):
         s.upload(l + 1, M.capi.X, coarse)
         s.interpolate(l)
         assert relmax(s.download(l, M.capi.X), o.interpolate(l, coarse)) < tol, l
+
+
+@pytest.mark.parametrize("shape,tensor", [
+    ((64, 64, 64), "full"), ((40, 70, 130), "full"), ((97, 33, 65), "full"), ((33, 65, 129), "iso"),
+    ((70, 40, 66), "diag"), ((130, 66, 24), "full"), ((18, 20, 3), "iso"), ((16, 17, 23), "full"),
+])
+@pytest.mark.parametrize("cycle", [0, 2])  # 2 (SMOOTHER): level-0 records carry b
+def test_residual_restriction_one_pass_is_bitwise(shape, tensor, prec, cycle):
+    """resid_restrict3_k (the V-cycle descent b_c = R (b - A x) without storing r) equals
+    mad_residual + mad_restrict bit for bit on every level it applies to: partial tiles,
+    odd (vertex-centred) and even (cell-centred) axes, chunked coarse planes."""
+    import multigridanisotropicdiffusion_amd as M
+    import synth
+    T = {"full": lambda: synth.random_spd(shape, seed=1),
+         "diag": lambda: synth.random_spd(shape, seed=1, offdiag=False),
+         "iso": lambda: synth.isotropic(shape)}[tensor]()
+    s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec, cycle=cycle)
+    s.set_tensor(T)
+    s.setup()
+    rng = np.random.default_rng(3)
+    nfused = 0
+    for l in range(s.num_levels - 1):
+        s.upload(l, M.capi.X, rng.standard_normal(s.shape_at(l)))
+        s.upload(l, M.capi.B, rng.standard_normal(s.shape_at(l)))
+        s.residual(l)
+        s.restrict(l)
+        ref = s.download(l + 1, M.capi.B)
+        s.upload(l + 1, M.capi.B, np.full(s.shape_at(l + 1), 7.0))
+        nfused += s.residual_restrict(l)
+        got = s.download(l + 1, M.capi.B)
+        assert np.array_equal(got, ref), (l, np.abs(got - ref).max())
+    if s.num_levels > 1 and min(s.shape_at(0)[1:]) >= 16:
+        assert nfused >= 1
