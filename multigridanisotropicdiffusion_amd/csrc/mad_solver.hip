@@ -939,10 +939,16 @@ class Solver final : public SolverBase {
     }();
     static const int target = [] {
       const char* e = std::getenv("MAD_RR_BLOCKS");  // tuning runs only
-      return e ? std::max(1, std::atoi(e)) : 512;
+      return e ? std::max(1, std::atoi(e)) : 1024;
     }();
-    auto run = [&](auto CXc, auto CYc) {
-      constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = 1024;
+    // 512-thread blocks, two per CU (one block's barriers overlap the other's loads):
+    // 1.133 vs 1.177 ms per 512^3 launch at 1024 blocks (profiles/r01_rr_nt_prof.log)
+    static const int nt = [] {
+      const char* e = std::getenv("MAD_RR_NT");  // tuning runs only: 512 or 1024 threads
+      return e ? std::atoi(e) : 512;
+    }();
+    auto run = [&](auto CXc, auto CYc, auto NTc) {
+      constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = decltype(NTc)::value;
       const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
       int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / 4));
       const int kc = (C.g.nz + chunks - 1) / chunks;
@@ -963,9 +969,14 @@ class Solver final : public SolverBase {
       else go(std::integral_constant<int, KISO>{});
     };
     if (tile == 1)
-      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 16>{});
+      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 16>{},
+          std::integral_constant<int, 1024>{});
+    else if (nt == 512)
+      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
+          std::integral_constant<int, 512>{});
     else
-      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{});
+      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
+          std::integral_constant<int, 1024>{});
     HIP_CHECK(hipGetLastError());
     return true;
   }
