@@ -3,7 +3,9 @@
 # block shape (rocprofv3 kernel trace; the stats CSV holds the average per kernel)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for cfg in "1024 512" "512 1024" "512 512" "1024 1024"; do
+CFGS=${CFGS:-"1024 512|512 1024|512 512|1024 1024"}
+IFS="|" read -ra LIST <<< "$CFGS"
+for cfg in "${LIST[@]}"; do
   set -- $cfg
   MAD_RR_NT=$1 MAD_RR_BLOCKS=$2 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rr_$1_$2 -o run -- python3 bench.py --steps 3 --warmup 1 --vcycles 20 --no-cpu-baseline > /dev/null 2>&1
   f=$(find gpurun_out/prof_rr_$1_$2 -name "*kernel_stats.csv" | head -1)
