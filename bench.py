@@ -9,9 +9,15 @@ generated on the device), dt 0.1, unit spacing, 4-colour Gauss-Seidel smoother.
 One step = one level-0 smoother sweep (all colours) over the whole volume.
 
     python bench.py [--gpus N --steps K --warmup W]
-For N > 1 the driver launches one process per GPU (torch.distributed.run);
-the volume is split into z-slabs (strong scaling, fixed 512^3) with RCCL halo
-exchanges.  Rank 0 prints one JSON line.
+bench.py itself starts no processes: for N > 1 it must run under
+torch.distributed.run with one process per GPU (WORLD_SIZE = N; --gpus must
+match it, or the run exits with an error).  The volume is split into z-slabs
+(strong scaling, fixed 512^3) with RCCL halo exchanges.  Rank 0 prints one
+JSON line.
+
+V-cycles/s are measured on a second solver built like a real solve
+(CycleType VCYCLE: dense rhs layout, the production V-cycle), not on the
+SMOOTHER-mode solver of the sweep measurement.
 """
 import argparse
 import json
@@ -41,6 +47,18 @@ def parse():
     return p.parse_args()
 
 
+def cpu_model():
+    """The host CPU's model name (lscpu's 'Model name', read from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(seconds):
     """fp64 oracle (restated reference algorithm, lexicographic GS, 1 thread) on a
     bounded 128^3 sample of the same VED-form workload."""
@@ -64,6 +82,7 @@ def cpu_baseline(seconds):
             break
     nvox = float(np.prod(shape))
     out = {"value": nvox * n / el / 1e6, "unit": "Mvoxel-smooths/s", "cores": 1, "kind": "port",
+           "cpu_model": cpu_model(),
            "sample": f"128^3 VED-form full tensor, {n} lexicographic GS sweeps, fp64, "
                      f"oracle/ (line-faithful restatement of the ITK reference), {el:.1f} s"}
     # beside it: the same restatement's multicolour GS (the GPU's sweep order) on the host
@@ -102,7 +121,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = max(a.gpus, world)
+    if a.gpus != world:
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch N > 1 GPUs with "
+                 "python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+    n_gpus = world
     dist = None
     if world > 1:
         # one node (the contract launches --nnodes=1): RCCL's bootstrap stays on loopback,
@@ -158,7 +180,25 @@ def main():
         wall = float(tt[0])
     nvox = float(S) ** 3
     value = nvox * a.steps / wall / 1e6
-    # V-cycles/s (same volume, nu = 2)
+    info = s.level_info(0)
+    nlev = s.num_levels
+    kname = s.smooth_kernel_name(0)  # as rocprofv3 prints it (profiles/ are matched on it)
+    s.close()
+    # V-cycles/s (same volume, nu = 2) on a solver in the production layout (CycleType
+    # VCYCLE: level-0 records without b, dense rhs), as GenerateData runs it
+    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
+                 cycle=M.VCYCLE,
+                 nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
+                 gs_kernel=a.gs_kernel)
+    if world > 1:
+        uid = M.comm_unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, src=0)
+        s.comm_init(bytes(t.tolist()))
+    s.synth_tensor(kind=0, seed=4)
+    s.setup()
+    s.synth_level(0, M.capi.B, 3)
+    s.synth_level(0, M.capi.X, 3)
     s.vcycle()
     barrier()
     t1 = time.perf_counter()
@@ -170,8 +210,7 @@ def main():
         tt = torch.tensor([vwall], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         vwall = float(tt[0])
-    info = s.level_info(0)
-    nlev = s.num_levels
+    s.close()
 
     if rank != 0:
         if dist is not None:
@@ -183,7 +222,6 @@ def main():
     units_per_launch = float(shape[0] * shape[1] * shape[2]) * a.steps / max(1, launches)
     achieved = BYTES_PER_VOXEL_SMOOTH * units_per_launch / (kern_ms * 1e-3) / 1e9
     tag = f"{a.smoother}_{S}"
-    kname = s.smooth_kernel_name(0)  # as rocprofv3 prints it (profiles/ are matched on it)
     traffic = load_traffic(tag, kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
@@ -217,6 +255,9 @@ def main():
                    "levels": nlev, "time_step": 0.1, "parallelism": f"z-slab x{world}",
                    "slab_shape": list(info["shape"])},
         "vcycles_per_s": round(a.vcycles / vwall, 3),
+        "vcycle_config": "CycleType VCYCLE (dense rhs layout), nu = 2, 4-colour GS, "
+                         f"{nlev} levels, graph-replayed per rank",
+        "device_ms_per_vcycle": round(vc_ms / a.vcycles, 3),
         "ms_per_vcycle": round(vwall / a.vcycles * 1e3, 3),
         "device_ms_per_step": round(dev_ms / a.steps, 4),
         "roofline": roof,

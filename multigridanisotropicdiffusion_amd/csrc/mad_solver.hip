@@ -1131,6 +1131,20 @@ class Solver final : public SolverBase {
       return;
     }
     sync_brec(0);  // eager: level 0's b changes between cycles (time steps), not inside
+    if (vgraph_) {
+      // the graph baked in every level's x / t buffers: a call between two cycles that
+      // swapped a ping-pong pair an odd number of times (mad_smooth with an odd sweep
+      // count under WJ, or of the fused GS sweep) leaves it pointing at stale buffers,
+      // so it is re-captured for the current pointers
+      bool same = vgraph_ptrs_.size() == lv_.size();
+      for (size_t l = 0; same && l < lv_.size(); ++l)
+        same = vgraph_ptrs_[l].first == lv_[l].x && vgraph_ptrs_[l].second == lv_[l].t;
+      if (!same) {
+        HIP_CHECK(hipStreamSynchronize(c_->stream));
+        (void)hipGraphExecDestroy(vgraph_);
+        vgraph_ = nullptr;
+      }
+    }
     if (!vgraph_) {
       struct Snap {
         T* x;
@@ -1180,6 +1194,8 @@ class Solver final : public SolverBase {
         vcycle_rec(0);
         return;
       }
+      vgraph_ptrs_.clear();
+      for (auto& L : lv_) vgraph_ptrs_.emplace_back(L.x, L.t);
     }
     HIP_CHECK(hipGraphLaunch(vgraph_, c_->stream));
     for (size_t l = 1; l < lv_.size(); ++l) lv_[l].b_halo_ok = lv_[l].brec_ok = false;  // as eager
@@ -1244,6 +1260,8 @@ class Solver final : public SolverBase {
         x_changed(0);
       }
       const double rhsNorm = norm(0, MAD_B);  // MAD.hxx:204
+      REQUIRE(std::isfinite(rhsNorm), MAD_ERR_NUMERIC,
+              "non-finite right-hand side norm (NaN/Inf in the input image)");
       unsigned it = 0;
       double best = INFINITY;
       std::vector<double> hist;
@@ -1256,7 +1274,13 @@ class Solver final : public SolverBase {
           if (d.verbose && c_->comm.rank() == 0) std::printf("\n|--- VCycle n. %u ---|\n", it + 1);
           vcycle_fast();
         }
-        relres = residual_impl(0, true, false) / rhsNorm;  // MAD.hxx:221-229 (norm only)
+        const double resNorm = residual_impl(0, true, false);  // MAD.hxx:221-229 (norm only)
+        // NaN > tol is false: without this check a NaN residual ends the do/while as if
+        // converged and the call returns MAD_OK with a NaN image
+        REQUIRE(std::isfinite(resNorm), MAD_ERR_NUMERIC,
+                "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
+        // an all-zero image (rhsNorm 0) is its own solution: report relres 0, not 0/0
+        relres = (rhsNorm > 0.0) ? resNorm / rhsNorm : resNorm;
         if (d.verbose && d.cycle == MAD_SMOOTHER && c_->comm.rank() == 0)
           std::printf("Smoother iteration n. %u: relative residual = %g\n", it + 1, relres);
         ++it;
@@ -1397,6 +1421,7 @@ class Solver final : public SolverBase {
   std::vector<LevelData<T>> lv_;
   int64_t part_cap_ = 0;             // entries of part_
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
+  std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
   bool vgraph_failed_ = false;
   int ncoef_ = 0;
   double* part_ = nullptr;
@@ -1414,6 +1439,7 @@ class Solver final : public SolverBase {
     if (c_ && c_->comm_stream) (void)hipStreamSynchronize(c_->comm_stream);
     if (vgraph_) (void)hipGraphExecDestroy(vgraph_);
     vgraph_ = nullptr;
+    vgraph_ptrs_.clear();
     vgraph_failed_ = false;
     for (auto& L : lv_) {
       if (L.ev_bnd) (void)hipEventDestroy(L.ev_bnd);

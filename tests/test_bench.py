@@ -46,3 +46,13 @@ def test_bench_json_line(extra):
     assert r["launches"] == 4 * nl
     assert r["algorithmic_bytes_per_launch"] == 36.0 * 256 ** 3 / nl
     assert 0 < r["kernel_ms_min"] <= r["kernel_ms_median"]
+
+
+def test_gpus_must_match_world_size():
+    """bench.py starts no processes: --gpus N without N launched ranks is an error, not
+    a 1-GPU run reported as N GPUs."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                         capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
