@@ -125,16 +125,14 @@ def main():
         sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch N > 1 GPUs with "
                  "python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
     n_gpus = world
-    dist = None
-    if world > 1:
-        # one node (the contract launches --nnodes=1): RCCL's bootstrap stays on loopback,
-        # the halos go GPU to GPU over xGMI
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        os.environ.setdefault("NCCL_DEBUG", "WARN")
-        import torch  # noqa: F401  (torch first: our library then binds to the same HIP runtime)
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+    # N > 1: one node (the contract launches --nnodes=1).  No torch in this process: the
+    # ranks meet through a file keyed by their common launcher (distributed.bootstrap_node)
+    # and synchronise over the solver's own RCCL communicator, so libmad_hip.so binds the
+    # ROCm RCCL it was compiled against (torch would bring its own librccl.so.1 first).
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
     import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as MD
 
     S = a.size
     gshape = (S, S, S)
@@ -148,11 +146,7 @@ def main():
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
                  gs_kernel=a.gs_kernel)
     if world > 1:
-        import torch
-        uid = M.comm_unique_id() if rank == 0 else bytes(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, src=0)
-        s.comm_init(bytes(t.tolist()))
+        MD.bootstrap_node(s, rank, world, tag="sweep")
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
@@ -161,8 +155,8 @@ def main():
 
     def barrier():
         s.synchronize()
-        if dist is not None:
-            dist.barrier()
+        if world > 1:
+            s.allreduce([0.0])
 
     # warmup
     if a.warmup:
@@ -173,11 +167,8 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     per_launch = sorted(s.bench_launch_times())
-    if dist is not None:
-        import torch
-        tt = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt[0])
+    if world > 1:
+        wall = float(s.allreduce([wall], "max")[0])
     nvox = float(S) ** 3
     value = nvox * a.steps / wall / 1e6
     info = s.level_info(0)
@@ -191,10 +182,7 @@ def main():
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
                  gs_kernel=a.gs_kernel)
     if world > 1:
-        uid = M.comm_unique_id() if rank == 0 else bytes(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, src=0)
-        s.comm_init(bytes(t.tolist()))
+        MD.bootstrap_node(s, rank, world, tag="vcycle")
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
@@ -205,16 +193,11 @@ def main():
     vc_ms = s.bench_vcycle(a.vcycles)
     barrier()
     vwall = time.perf_counter() - t1
-    if dist is not None:
-        import torch
-        tt = torch.tensor([vwall], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        vwall = float(tt[0])
+    if world > 1:
+        vwall = float(s.allreduce([vwall], "max")[0])
     s.close()
 
     if rank != 0:
-        if dist is not None:
-            dist.barrier()
         return
     # roofline of the dominant kernel: voxel updates per launch from the launch count the
     # library reports (the fused GS / WJ sweep: the whole slab per launch; per-colour GS
@@ -268,8 +251,6 @@ def main():
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.barrier()
 
 
 if __name__ == "__main__":

@@ -42,7 +42,7 @@ typedef enum mad_status {
   MAD_ERR_SINGULAR = 5,    /* coarsest operator singular */
   MAD_ERR_UNSUPPORTED = 6, /* valid request this build does not implement */
   MAD_ERR_NOMEM = 7,
-  MAD_ERR_NUMERIC = 8      /* NaN/Inf residual */
+  MAD_ERR_NUMERIC = 8      /* NaN/Inf residual norm or diffusion tensor */
 } mad_status;
 
 /* MAD.h:123 enum CycleType { VCYCLE, FMG, SMOOTHER } -- same values */
@@ -234,9 +234,19 @@ int mad_comm_init(mad_ctx *ctx, const void *uid128);
 int mad_comm_init_local(mad_ctx *ctx, uint64_t group);
 /* Transport self-test on one GPU: a single-rank RCCL communicator runs the halo
  * exchange (grouped ncclSend/ncclRecv, both neighbours = this rank), the fp64
- * allreduce and the slab allgather the solver uses, on `device`; *max_err is the
- * largest deviation from the expected bytes (0 when the transport works). */
+ * allreduce and the slab allgather the solver uses, on `device`, first eagerly and
+ * then captured into a hipGraph and replayed twice (the multi-rank V-cycle graph
+ * holds these operations); *max_err is the largest deviation from the expected
+ * bytes over all runs (0 when the transport works). */
 int mad_comm_selftest(int32_t device, double *max_err);
+/* Host values reduced over the ranks of ctx's communicator (op 0 = sum, 1 = max),
+ * in place; a barrier as a side effect.  Lets a host program (bench.py) synchronise
+ * ranks and take its max-over-ranks timing over the solver's own RCCL communicator. */
+int mad_comm_allreduce_host(mad_ctx *ctx, double *values, uint32_t n, int32_t op);
+/* RCCL version the process bound at run time, and NCCL_VERSION_CODE of the headers
+ * the library was compiled with (major*10000 + minor*100 + patch).  mad_comm_init
+ * fails with MAD_ERR_COMM when their major.minor differ. */
+int mad_comm_version(int32_t *runtime, int32_t *compiled);
 /* slab [z_begin, z_end) of this rank for a global nz (even-aligned split) */
 int mad_slab_range(int64_t nz, int32_t nranks, int32_t rank, int32_t align, int64_t *z_begin,
                    int64_t *z_end);

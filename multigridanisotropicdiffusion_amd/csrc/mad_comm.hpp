@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -99,14 +100,31 @@ class Comm {
   void init(const void* uid128, int nranks, int rank, int device) {
     destroy();
     if (nranks <= 1) return;
-    init_rccl(uid128, nranks, rank);
-    (void)device;
+    init_rccl(uid128, nranks, rank, device);
+  }
+
+  // RCCL the process bound at run time (major * 10000 + minor * 100 + patch); a
+  // process that loaded another librccl.so.1 first (torch bundles its own) binds that one
+  static int runtime_version() {
+    int v = 0;
+    NCCL_CHECK(ncclGetVersion(&v));
+    return v;
   }
 
   // an RCCL communicator of any size, one rank included (the transport self-test,
-  // mad_comm_selftest: a single-rank communicator exchanges with itself)
-  void init_rccl(const void* uid128, int nranks, int rank) {
+  // mad_comm_selftest: a single-rank communicator exchanges with itself).  The
+  // communicator lives on `device` (>= 0; -1 keeps the current device).
+  void init_rccl(const void* uid128, int nranks, int rank, int device = -1) {
     destroy();
+    // the library is compiled against the ROCm RCCL headers: refuse a runtime library of
+    // another major.minor (argument structs and enum values may differ between them)
+    const int v = runtime_version();
+    if (v / 100 != NCCL_VERSION_CODE / 100)
+      throw CommError("RCCL runtime " + std::to_string(v) + " does not match the headers the "
+                      "library was built with (" + std::to_string(NCCL_VERSION_CODE) +
+                      "): load libmad_hip.so before anything that brings its own librccl "
+                      "(e.g. import torch)");
+    if (device >= 0) HIPC_CHECK(hipSetDevice(device));
     ncclUniqueId id;
     std::memcpy(&id, uid128, sizeof(id));
     NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
@@ -135,6 +153,7 @@ class Comm {
   }
 
   bool active() const { return mode_ != NONE && nranks_ > 1; }
+  Mode mode() const { return mode_; }
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
 
@@ -195,6 +214,30 @@ class Comm {
     group_->barrier();
     HIPC_CHECK(hipMemcpyAsync(p, &sum, sizeof(double), hipMemcpyHostToDevice, s));
     HIPC_CHECK(hipStreamSynchronize(s));
+  }
+
+  // host-side reduction of n doubles over the ranks (op 0 sum, 1 max), through a device
+  // buffer on stream s: the bench's barrier and max-over-ranks timing without torch
+  void allreduce_host(double* v, size_t n, int op, hipStream_t s) {
+    if (mode_ == RCCL) {
+      double* d = nullptr;
+      HIPC_CHECK(hipMalloc(&d, sizeof(double) * n));
+      HIPC_CHECK(hipMemcpyAsync(d, v, sizeof(double) * n, hipMemcpyHostToDevice, s));
+      NCCL_CHECK(ncclAllReduce(d, d, n, ncclDouble, op ? ncclMax : ncclSum, comm_, s));
+      HIPC_CHECK(hipMemcpyAsync(v, d, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+      HIPC_CHECK(hipStreamSynchronize(s));
+      HIPC_CHECK(hipFree(d));
+      return;
+    }
+    if (mode_ != LOCAL) return;  // one rank: nothing to reduce
+    for (size_t q = 0; q < n; ++q) {
+      group_->val[rank_] = v[q];
+      group_->barrier();
+      double r = group_->val[0];
+      for (int k = 1; k < nranks_; ++k) r = op ? std::max(r, group_->val[k]) : r + group_->val[k];
+      group_->barrier();
+      v[q] = r;
+    }
   }
 
   // every rank holds nz_global / nranks planes; gather all slabs in rank order

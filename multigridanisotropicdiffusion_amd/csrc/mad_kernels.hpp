@@ -1823,10 +1823,12 @@ __global__ void __launch_bounds__(256) aos_to_soa_k(const S* __restrict__ in, do
     for (int c = 0; c < ncomp; ++c) out[c * n + q] = (double)in[q * ncomp + c];
 }
 
-// flags[0] += any off-diagonal != 0, flags[1] += any diagonal entries differ
+// flags[0] += any off-diagonal != 0, flags[1] += any diagonal entries differ,
+// flags[2] += any entry non-finite (NaN / Inf: MAD_ERR_NUMERIC at setup)
 __global__ void __launch_bounds__(256) tensor_kind_k(const double* __restrict__ M, int64_t n, int dim,
                                                      unsigned int* __restrict__ flags) {
-  unsigned int off = 0, aniso = 0;
+  unsigned int off = 0, aniso = 0, bad = 0;
+  const int ncomp = dim * (dim + 1) / 2;
   for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
        q += (int64_t)gridDim.x * blockDim.x) {
     if (dim == 3) {
@@ -1836,9 +1838,11 @@ __global__ void __launch_bounds__(256) tensor_kind_k(const double* __restrict__ 
       off |= (M[1 * n + q] != 0.0);
       aniso |= (M[0 * n + q] != M[2 * n + q]);
     }
+    for (int c = 0; c < ncomp; ++c) bad |= !isfinite(M[c * n + q]);
   }
   if (__any(off) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
   if (__any(aniso) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1u);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[2], 1u);
 }
 
 __device__ __forceinline__ int tcomp(int dim, int d, int d2) {

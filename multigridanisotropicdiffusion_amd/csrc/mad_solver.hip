@@ -1123,14 +1123,62 @@ class Solver final : public SolverBase {
   // cycle is ~40 launches per level and the coarse levels are launch-bound.  The
   // graph bakes in the array pointers, so it is only used when a cycle leaves the
   // ping-pong state (x <-> t swaps of the fused sweep) unchanged, i.e. an even
-  // number of fused sweeps per level; verbose runs and multi-rank runs (host-side
-  // transport, per-cycle exchanges) stay eager.
+  // number of fused sweeps per level, and re-captured when a call between cycles
+  // swapped a pair.  Verbose runs stay eager (host norms per sweep).
+  //
+  // Rank slabs over RCCL are captured too: the halo exchanges (grouped
+  // ncclSend/ncclRecv), the slab allgather of the agglomeration and the
+  // communication-stream overlap of the fused sweep (event fork / join) are all
+  // stream-ordered, so one graph per rank holds the whole cycle.  The host's
+  // ghost-plane bookkeeping is made canonical around the graph: level 0's x / b ghost
+  // planes are made current eagerly before every capture and replay (a no-op when they
+  // are), the cycle ends joined (no exchange left in flight), and the bookkeeping the
+  // capture left behind is re-applied after every replay.  The first multi-rank cycle
+  // runs eagerly (RCCL connects its peers lazily, outside any capture).  The
+  // in-process LOCAL transport synchronises on the host and stays eager, as does the
+  // wait-on-value single-launch sweep (gs_kernel 4); MAD_VGRAPH_RANKS=0 disables the
+  // multi-rank graph.
+  bool vgraph_ranks_ok() const {
+    static const bool env_ok = [] {
+      const char* e = std::getenv("MAD_VGRAPH_RANKS");
+      return !(e && e[0] == '0');
+    }();
+    return env_ok && c_->comm.mode() == Comm::RCCL && c_->d.gs_kernel != 4;
+  }
+
+  struct HaloFlags {
+    bool x_ok, b_ok, brec_ok;
+  };
+  std::vector<HaloFlags> halo_flags() const {
+    std::vector<HaloFlags> v;
+    for (auto& L : lv_) v.push_back({L.x_halo_ok, L.b_halo_ok, L.brec_ok});
+    return v;
+  }
+  // canonical entry state of a multi-rank graph cycle (host bookkeeping + level 0's
+  // ghost planes made current on the stream)
+  void ranks_graph_entry() {
+    halo(0, lv_[0].x, GHOST);
+    if (!lv_[0].brec && !lv_[0].b_halo_ok) {
+      halo(0, lv_[0].b, GHOST);
+      lv_[0].b_halo_ok = true;
+    }
+    wait_all_pending();
+    for (size_t l = 1; l < lv_.size(); ++l) {
+      lv_[l].x_halo_ok = false;
+      lv_[l].b_halo_ok = lv_[l].brec_ok = false;
+    }
+  }
+
   void vcycle_fast() {
-    if (c_->d.verbose || c_->comm.active() || vgraph_failed_) {
+    const bool ranks = c_->comm.active();
+    if (c_->d.verbose || vgraph_failed_ || (ranks && !vgraph_ranks_ok()) ||
+        (ranks && vcycles_eager_ < 1)) {
+      if (ranks) ++vcycles_eager_;
       vcycle_rec(0);
       return;
     }
     sync_brec(0);  // eager: level 0's b changes between cycles (time steps), not inside
+    if (ranks) ranks_graph_entry();
     if (vgraph_) {
       // the graph baked in every level's x / t buffers: a call between two cycles that
       // swapped a ping-pong pair an odd number of times (mad_smooth with an odd sweep
@@ -1168,28 +1216,46 @@ class Solver final : public SolverBase {
         }
       };
       const std::vector<Snap> before = snap();
+      const std::vector<HaloFlags> flags_before = halo_flags();
       hipGraph_t gph = nullptr;
       HIP_CHECK(hipStreamBeginCapture(c_->stream, hipStreamCaptureModeThreadLocal));
+      bool captured = true;
       try {
         vcycle_rec(0);
+        if (ranks) wait_all_pending();  // join the communication stream: no open branch
       } catch (...) {
         (void)hipStreamEndCapture(c_->stream, &gph);
         if (gph) (void)hipGraphDestroy(gph);
+        gph = nullptr;
         restore(before);
-        throw;
+        if (!ranks) throw;
+        captured = false;  // a transport that refuses capture: eager from here on
       }
-      HIP_CHECK(hipStreamEndCapture(c_->stream, &gph));
+      if (captured && hipStreamEndCapture(c_->stream, &gph) != hipSuccess) {
+        gph = nullptr;
+        captured = false;
+      }
       const std::vector<Snap> after = snap();
-      bool same = true;
-      for (size_t l = 0; l < before.size(); ++l)
-        same = same && before[l].x == after[l].x && before[l].t == after[l].t;
+      bool same = captured;
+      for (size_t l = 0; same && l < before.size(); ++l)
+        same = before[l].x == after[l].x && before[l].t == after[l].t;
+      vgraph_exit_flags_ = halo_flags();  // the bookkeeping one cycle leaves
       restore(before);  // capture issued nothing: the state must not advance
+      if (ranks) {
+        for (size_t l = 0; l < lv_.size(); ++l) {
+          lv_[l].x_halo_ok = flags_before[l].x_ok;
+          lv_[l].b_halo_ok = flags_before[l].b_ok;
+          lv_[l].brec_ok = flags_before[l].brec_ok;
+          lv_[l].x_halo_pending = false;
+        }
+      }
       if (same && hipGraphInstantiate(&vgraph_, gph, nullptr, nullptr, 0) != hipSuccess) {
         vgraph_ = nullptr;
         same = false;
       }
-      (void)hipGraphDestroy(gph);
+      if (gph) (void)hipGraphDestroy(gph);
       if (!same) {
+        (void)hipGetLastError();
         vgraph_failed_ = true;
         vcycle_rec(0);
         return;
@@ -1198,7 +1264,16 @@ class Solver final : public SolverBase {
       for (auto& L : lv_) vgraph_ptrs_.emplace_back(L.x, L.t);
     }
     HIP_CHECK(hipGraphLaunch(vgraph_, c_->stream));
-    for (size_t l = 1; l < lv_.size(); ++l) lv_[l].b_halo_ok = lv_[l].brec_ok = false;  // as eager
+    if (ranks) {
+      for (size_t l = 0; l < lv_.size(); ++l) {
+        lv_[l].x_halo_ok = vgraph_exit_flags_[l].x_ok;
+        lv_[l].b_halo_ok = vgraph_exit_flags_[l].b_ok;
+        lv_[l].brec_ok = vgraph_exit_flags_[l].brec_ok;
+        lv_[l].x_halo_pending = false;
+      }
+    } else {
+      for (size_t l = 1; l < lv_.size(); ++l) lv_[l].b_halo_ok = lv_[l].brec_ok = false;  // as eager
+    }
   }
 
   void vcycle() override { vcycle_fast(); }
@@ -1423,6 +1498,8 @@ class Solver final : public SolverBase {
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
   std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
   bool vgraph_failed_ = false;
+  std::vector<HaloFlags> vgraph_exit_flags_;  // rank slabs: ghost bookkeeping after one cycle
+  int vcycles_eager_ = 0;  // rank slabs: cycles run eagerly so far (RCCL peers connected)
   int ncoef_ = 0;
   double* part_ = nullptr;
   double* scal_ = nullptr;
@@ -1441,6 +1518,7 @@ class Solver final : public SolverBase {
     vgraph_ = nullptr;
     vgraph_ptrs_.clear();
     vgraph_failed_ = false;
+    vcycles_eager_ = 0;
     for (auto& L : lv_) {
       if (L.ev_bnd) (void)hipEventDestroy(L.ev_bnd);
       if (L.ev_halo) (void)hipEventDestroy(L.ev_halo);
@@ -2003,22 +2081,23 @@ static void setup_impl(mad_ctx* c) {
   const LevelGeom& G = c->geom[0];
   const int ncomp = c->dim * (c->dim + 1) / 2;
   (void)ncomp;
-  // resolve the tensor kind
+  // resolve the tensor kind, and reject a non-finite tensor (it would surface later as
+  // a singular coarsest operator or a NaN image)
   int kind = KFULL;
-  if (c->d.tensor_kind == MAD_TENSOR_AUTO) {
+  {
     unsigned int* flags = nullptr;
-    HIP_CHECK(hipMalloc(&flags, sizeof(unsigned int) * 2));
-    HIP_CHECK(hipMemsetAsync(flags, 0, sizeof(unsigned int) * 2, c->stream));
+    HIP_CHECK(hipMalloc(&flags, sizeof(unsigned int) * 3));
+    HIP_CHECK(hipMemsetAsync(flags, 0, sizeof(unsigned int) * 3, c->stream));
     hipLaunchKernelGGL(tensor_kind_k, dim3(flat_blocks(G.N, 2048)), dim3(256), 0, c->stream,
                        c->tensor64, G.N, c->dim, flags);
     HIP_CHECK(hipGetLastError());
-    unsigned int hf[2];
+    unsigned int hf[3];
     HIP_CHECK(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     HIP_CHECK(hipFree(flags));
-    kind = hf[0] ? KFULL : (hf[1] ? KDIAG : KISO);
-  } else {
-    kind = c->d.tensor_kind;  // MAD_TENSOR_* == KISO/KDIAG/KFULL
+    REQUIRE(hf[2] == 0, MAD_ERR_NUMERIC, "diffusion tensor has non-finite (NaN / Inf) entries");
+    if (c->d.tensor_kind == MAD_TENSOR_AUTO) kind = hf[0] ? KFULL : (hf[1] ? KDIAG : KISO);
+    else kind = c->d.tensor_kind;  // MAD_TENSOR_* == KISO/KDIAG/KFULL
   }
   c->kind = kind;
   c->ncolors = (kind == KFULL) ? 4 : 2;
@@ -2028,6 +2107,14 @@ static void setup_impl(mad_ctx* c) {
   }
   c->solver->setup(c);
   c->setup_done = true;
+  if (c->d.nranks > 1) {
+    // a rank slab's setup works on the global fp64 tensor (replicated operator build);
+    // once the slab's operators exist it is dead weight (26 GB at 1024 x 1024 x 512), so
+    // it is released -- the next setup needs a new mad_set_tensor, as after construction
+    HIP_CHECK(hipFree(c->tensor64));
+    c->tensor64 = nullptr;
+    c->tensor_set = false;
+  }
   c->setup_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -2292,12 +2379,60 @@ int mad_comm_selftest(int32_t device, double* max_err) {
     }
     for (size_t q = 0; q < og.size(); ++q)
       err = std::max(err, (double)std::fabs(og[q] - h[(size_t)GHOST * P + q]));
+    // the same three operations captured into a hipGraph and replayed (the multi-rank
+    // V-cycle graph holds them, vcycle_fast): inputs reset, outputs cleared first
+    {
+      hipGraph_t gph = nullptr;
+      hipGraphExec_t gx = nullptr;
+      HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      comm.exchange_planes(base, P, NZ, GHOST, 1, 1, sizeof(float), false, s);
+      comm.allreduce_sum_f64(v, 1, s);
+      comm.allgather_slabs(base, g, P, NZ, sizeof(float), s);
+      HIP_CHECK(hipStreamEndCapture(s, &gph));
+      HIP_CHECK(hipGraphInstantiate(&gx, gph, nullptr, nullptr, 0));
+      for (int rep = 0; rep < 2; ++rep) {
+        HIP_CHECK(hipMemcpy(d, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(v, &one, sizeof one, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemset(g, 0, sizeof(float) * (size_t)NZ * P));
+        HIP_CHECK(hipGraphLaunch(gx, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        HIP_CHECK(hipMemcpy(o.data(), d, sizeof(float) * o.size(), hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(og.data(), g, sizeof(float) * og.size(), hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(&vr, v, sizeof vr, hipMemcpyDeviceToHost));
+        err = std::max(err, std::fabs(vr - one));
+        for (int z = 0; z < NT; ++z) {
+          const int src = z < GHOST ? GHOST + z : (z >= NZ + GHOST ? z - GHOST : z);
+          for (int e = 0; e < P; ++e)
+            err = std::max(err, (double)std::fabs(o[(size_t)z * P + e] - h[(size_t)src * P + e]));
+        }
+        for (size_t q = 0; q < og.size(); ++q)
+          err = std::max(err, (double)std::fabs(og[q] - h[(size_t)GHOST * P + q]));
+      }
+      (void)hipGraphExecDestroy(gx);
+      (void)hipGraphDestroy(gph);
+    }
     *max_err = err;
     comm.destroy();
     (void)hipFree(d);
     (void)hipFree(v);
     (void)hipFree(g);
     (void)hipStreamDestroy(s);
+  });
+}
+
+int mad_comm_allreduce_host(mad_ctx* c, double* values, uint32_t n, int32_t op) {
+  if (!c || (!values && n) || (op != 0 && op != 1)) return MAD_ERR_INVALID;
+  return guarded(c, [&] {
+    use_device(c);
+    c->comm.allreduce_host(values, n, op, c->stream);
+  });
+}
+
+int mad_comm_version(int32_t* runtime, int32_t* compiled) {
+  if (!runtime || !compiled) return MAD_ERR_INVALID;
+  return guarded(nullptr, [&] {
+    *runtime = Comm::runtime_version();
+    *compiled = NCCL_VERSION_CODE;
   });
 }
 

@@ -4,16 +4,25 @@ The decomposition itself lives in the C++ library (plan_geometry in
 csrc/mad_solver.hip, transports in csrc/mad_comm.hpp).  This module only
 bootstraps it:
 
-* ``bootstrap_rccl(solver, dist)`` -- rank 0 creates the RCCL unique id and
-  broadcasts it over an initialised torch.distributed process group (gloo is
-  enough: 128 bytes, once), then every rank joins the communicator.
+* ``bootstrap_node(solver, rank, world, tag)`` -- torch-free rendezvous on one
+  node: rank 0 creates the RCCL unique id and publishes it in a file keyed by the
+  launcher (the parent process shared by all ranks under torch.distributed.run)
+  and MASTER_PORT; the other ranks read it, then every rank joins.  Importing
+  torch is then unnecessary -- torch bundles its own librccl.so.1 / HIP runtime,
+  and a process that loads it first binds libmad_hip.so to that RCCL
+  (mad_comm_init refuses a major.minor other than the headers').
+* ``bootstrap_rccl(solver, dist)`` -- the same over an initialised
+  torch.distributed process group (gloo is enough: 128 bytes, once).
 * ``run_local(nranks, body)`` -- runs ``nranks`` ranks as host threads of this
   process on one device with the in-process transport (tests / rehearsal).
 * ``slabs(global_shape, nranks)`` -- the level-0 slab of every rank, from the
   host-only planner (mad_plan_level).
 """
 import ctypes
+import os
+import tempfile
 import threading
+import time
 import zlib
 
 from . import _capi as C
@@ -46,6 +55,46 @@ def plan(global_shape, nranks=1, rank=0):
 
 def slabs(global_shape, nranks):
     return [(p[0]["z0"], p[0]["z1"]) for p in (plan(global_shape, nranks, r) for r in range(nranks))]
+
+
+def _rdzv_path(tag):
+    key = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}-{tag}"
+    return os.path.join(tempfile.gettempdir(), f"mad_rccl_uid_{key}")
+
+
+def bootstrap_node(solver, rank, world, tag="0", timeout=120.0):
+    """Join the RCCL communicator of `world` ranks on this node without torch.
+
+    `tag` must differ between the communicators one job creates.  Rank 0 writes
+    the 128-byte unique id atomically (tmp file + rename); the others poll for it.
+    ncclCommInitRank is collective, so once it returns on rank 0 every rank has
+    read the id and rank 0 removes the file."""
+    path = _rdzv_path(tag)
+    if rank == 0:
+        uid = comm_unique_id()
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+    else:
+        t0 = time.monotonic()
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    uid = f.read()
+                if len(uid) == 128:
+                    break
+            except FileNotFoundError:
+                pass
+            if time.monotonic() - t0 > timeout:
+                raise TimeoutError(f"rank {rank}: no RCCL unique id at {path} after {timeout} s")
+            time.sleep(0.01)
+    solver.comm_init(uid)
+    if rank == 0:
+        try:
+            os.remove(path)
+        except FileNotFoundError:
+            pass
 
 
 def bootstrap_rccl(solver, dist):

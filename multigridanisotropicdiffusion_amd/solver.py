@@ -123,6 +123,15 @@ class Solver:
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         self._check(self._L.mad_comm_init(self._ctx, buf))
 
+    def allreduce(self, values, op="sum"):
+        """Reduce host floats over the ranks of this solver's communicator (sum / max),
+        a barrier as a side effect (mad_comm_allreduce_host)."""
+        v = np.ascontiguousarray(np.atleast_1d(np.asarray(values, dtype=np.float64))).copy()
+        self._check(self._L.mad_comm_allreduce_host(
+            self._ctx, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), v.size,
+            {"sum": 0, "max": 1}[op]))
+        return v
+
     def comm_init_local(self, group):
         """In-process transport: contexts sharing `group` exchange slabs directly."""
         self._check(self._L.mad_comm_init_local(self._ctx, int(group)))
@@ -248,6 +257,13 @@ class Solver:
         t = ctypes.c_double()
         self._check(self._L.mad_bench_vcycle(self._ctx, cycles, ctypes.byref(t)))
         return t.value
+
+
+def comm_version():
+    """(runtime, compiled) RCCL version codes (major*10000 + minor*100 + patch)."""
+    r, c = ctypes.c_int32(), ctypes.c_int32()
+    C.check(C.load().mad_comm_version(ctypes.byref(r), ctypes.byref(c)))
+    return r.value, c.value
 
 
 def comm_unique_id():
