@@ -102,7 +102,10 @@ typedef struct mad_desc {
   int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep, v3),
                                     1 one launch per colour, 2 fused v2, 3 fused v3,
                                     4 fused v3 with the last z-chunk marched downward (the
-                                    rank-slab form, selectable on one GPU for parity) */
+                                    rank-slab form, selectable on one GPU for parity),
+                                    5 / 6 as 3 / 4 with g recomputed in-kernel from 24-B
+                                    tensor records (full tensor only; gs_fusedg_k: fewer
+                                    bytes, but latency-bound and slower today) */
   int32_t reserved[8];
 } mad_desc;
 

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <type_traits>
 #include <cstdint>
 
 namespace mad {
@@ -956,6 +957,480 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
         }
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// g recomputed in-kernel (declared here, defined with build_g_k below)
+template <typename T>
+__device__ __forceinline__ T gdelta(T fm2, T fm1, T f0, T fp1, T fp2, bool lo, bool hi);
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void g_combine(T dxax, T dyay, T dzaz, T dxexy, T dyexy, T dxexz,
+                                          T dzexz, T dyeyz, T dzeyz, T& gx, T& gy, T& gz);
+
+// Fused 4-colour GS sweep of the full 3D operator with g recomputed in-kernel.
+// Reads 24-B tensor records [a_x a_y a_z e_xy e_xz e_yz] (LevelData::ct: cidx point order,
+// GHOST planes like the coefficient records), the dense b and u; writes u out of place.
+// Per voxel-sweep that is the 36 algorithmic bytes (+ the tile halo, mostly L2 hits:
+// neighbouring tiles of one XCD run the same planes together) instead of the 40-48 B of
+// gs_fused3_k, whose records also carry g.  Bit-identical to gs_fused3_k and to per-colour
+// passes on records whose g is build_g_k's (same gdelta / g_combine on the same values).
+//
+// Schedule as gs_fused3_k: z-marching wavefront (step k: stage c updates colour c on plane
+// k-c), overlapped tiles with halo H = 4, a 6-plane LDS ring of u with the x/y mirror images
+// of the domain faces.  Mapping: one thread per 2x2 point block of the tile region
+// (RX x RY = (TX+8) x (TY+8)).  A block holds one point of every colour on every plane, so
+// every stage updates one point per thread, and the block's four records of a plane are
+// read together as a plane stream.  g of plane k needs the tensor of planes k-1..k+1: the
+// z-differences come from the thread's own columns (registers; plane k+1 is loaded one
+// step ahead), the x/y differences from an LDS exchange plane of the in-plane components
+// (a_x a_y e_xy e_xz e_yz of plane k; a block's own neighbours come from registers).  A
+// point's record (tensor, b, g) then waits in registers until its colour's stage, 0..3
+// steps later (at most 2.5 planes of records per block): registers, not LDS, bound the
+// tile.  Domain faces: the reference's one-sided differences (gdelta) from the exchange
+// plane (x/y) and from a reload of plane k-2 (top z face).
+template <int TX, int TY>
+struct FusedGGeom {
+  static constexpr int H = 4;
+  static constexpr int RX = TX + 2 * H, RY = TY + 2 * H;
+  static constexpr int BX = RX / 2, BY = RY / 2, NB = BX * BY;
+  static constexpr int HALF = BX;  // row: even-x half (BX points), then the odd-x half
+  // 2 * PITCH == BX (mod 32): the lanes of a wave (blocks in row-major order) address
+  // consecutive element slots modulo 32 -> conflict-free 4-B and 8-B LDS accesses
+  static constexpr int pitch() {
+    int p = 2 * HALF;
+    while ((2 * p - BX) % 32 != 0) ++p;
+    return p;
+  }
+  static constexpr int PITCH = pitch();
+  static constexpr int PLANE = RY * PITCH;
+  static constexpr int NP = 8;                      // u ring planes (6 in use; 8: slot = m & 7)
+  static constexpr int NXC = 5;                     // exchange components
+  static constexpr int XPLANE = (RY + 2) * PITCH;   // one component, rows -1 .. RY
+  static constexpr int ELEMS = NP * PLANE + NXC * XPLANE;
+};
+
+template <typename T, int TX, int TY, int NT, int MINW = NT / 256>
+__global__ void __launch_bounds__(NT, MINW) gs_fusedg_k(const T* __restrict__ uin, T* __restrict__ uout,
+                                                           const T* __restrict__ b, const T* __restrict__ ct,
+                                                           Geo g, int zc, int ntx, int nty, int zbase,
+                                                           int zstride, int flip_last,
+                                                           uint32_t* __restrict__ sig) {
+  constexpr int NC = 4;
+  using FG = FusedGGeom<TX, TY>;
+  constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, BX = FG::BX, NB = FG::NB;
+  constexpr int HALF = FG::HALF, PITCH = FG::PITCH, PLANE = FG::PLANE, NP = FG::NP;
+  constexpr int XPLANE = FG::XPLANE;
+  constexpr int RS = 6;  // tensor record
+  constexpr uint32_t TS = sizeof(T);
+  static_assert(TX % 4 == 0 && TY % 2 == 0, "2x2 blocks, even BX");
+  static_assert(NB <= NT, "one 2x2 block per thread");
+  extern __shared__ __align__(16) unsigned char fused_smem[];
+  T* const ring = reinterpret_cast<T*>(fused_smem);
+  T* const xb = ring + NP * PLANE + PITCH;  // exchange component c at c * XPLANE, rows -1 .. RY
+
+  int bid = blockIdx.x;
+  {
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = bid & 7, idx = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int tiles = ntx * nty;
+  const int chunk = bid / tiles;
+  const int tile = bid - chunk * tiles;
+  const int tyi = tile / ntx;
+  const int txi = tile - tyi * ntx;
+  const int rx0 = txi * TX - H;
+  const int ry0 = tyi * TY - H;
+  const int tid = threadIdx.x;
+  const bool has = tid < NB;
+  const int bx = has ? tid % BX : 0, by = has ? tid / BX : 0;
+  const int nx = g.nx, ny = g.ny, sy = (int)g.sy, hx0 = g.hx0;
+  const bool interior = rx0 >= 2 && rx0 + RX <= nx - 2 && ry0 >= 2 && ry0 + RY <= ny - 2;
+
+  const int p0 = zbase + chunk * zstride;
+  const int p1 = min(p0 + zc, g.nz);
+  const bool flip = flip_last != 0 && chunk == (int)(gridDim.x / tiles) - 1;
+  int64_t sz = g.sz;
+  int zlo_g = g.zlo_ghost, zhi_g = g.zhi_ghost, zpar = g.zoff;
+  int z0 = p0, z1 = p1;
+  if (flip) {
+    const int64_t top = (int64_t)(g.nz - 1) * g.sz;
+    uin += top;
+    uout += top;
+    b += top;
+    ct += top * RS;
+    sz = -g.sz;
+    zlo_g = g.zhi_ghost;
+    zhi_g = g.zlo_ghost;
+    zpar = g.zoff + g.nz - 1;
+    z0 = g.nz - p1;
+    z1 = g.nz - p0;
+  }
+  const int zlo = zlo_g ? -GHOST : 0;
+  const int zhi = zhi_g ? g.nz + GHOST : g.nz;
+  const int ulo = zlo_g ? -(GHOST - 1) : 0;
+  const int uhi = zhi_g ? g.nz + GHOST - 1 : g.nz;
+  const bool signals = sig != nullptr && z0 == 0 && zlo_g;
+  // first step with (k + zpar) even, so step k0 + u has plane parity u & 1
+  const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + zpar) & 1);
+  const int kend = z1 + NC - 2;
+
+  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
+
+  // per point s = ox + 2 oy of the block: u / b source and tensor-record byte offsets in
+  // a plane (mirrored outside the domain: in bounds, values unused), LDS element offset in
+  // a plane slot, face flags for the one-sided g differences, output offset
+  // (LDS offsets are one per thread plus a compile-time term per point; an output point
+  // lies in the domain, so its store offset is its unmirrored source offset)
+  uint32_t usrc[4], tof[4];
+  const int uo0 = 2 * by * PITCH + bx;
+  auto uofs = [&](int s) { return uo0 + (s >> 1) * PITCH + (s & 1) * HALF; };
+  uint32_t bflags = 0;  // 4 bits per point: x low, x high, y low, y high face
+  uint32_t omask = 0;   // bit s: point s is a tile-interior output point
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int ox = s & 1, oy = s >> 1;
+    const int li = 2 * bx + ox, lj = 2 * by + oy;
+    const int gi = rx0 + li, gj = ry0 + lj;
+    const int gim = interior ? gi : mirror(gi, nx), gjm = interior ? gj : mirror(gj, ny);
+    usrc[s] = (uint32_t)(gjm * sy + gim) * TS;
+    tof[s] = (uint32_t)(gjm * sy + (gim & 1) * hx0 + (gim >> 1)) * (TS * RS);
+    const bool dom = gi >= 0 && gi < nx && gj >= 0 && gj < ny;
+    if (dom && has)
+      bflags |= ((gi == 0 ? 1u : 0u) | (gi == nx - 1 ? 2u : 0u) | (gj == 0 ? 4u : 0u) |
+                 (gj == ny - 1 ? 8u : 0u)) << (4 * s);
+    const bool out = has && li >= H && li < H + TX && lj >= H && lj < H + TY && gi < nx && gj < ny;
+    omask |= (out ? 1u : 0u) << s;
+  }
+  // stage c at plane parity PM updates point s(c, PM) of the block; valid and ghost-image
+  // bits as in gs_fused3_k
+  uint32_t vmask = 0, gmask = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int PM = 0; PM < 2; ++PM) {
+      const int ox = (c & 1) ^ PM, oy = ((c >> 1) & 1) ^ PM;
+      const int li = 2 * bx + ox, lj = 2 * by + oy;
+      const int gi = rx0 + li, gj = ry0 + lj;
+      const bool ok = has && li >= c + 1 && li < RX - c - 1 && lj >= c + 1 && lj < RY - c - 1 &&
+                      gi >= 0 && gi < nx && gj >= 0 && gj < ny;
+      vmask |= (ok ? 1u : 0u) << (c * 2 + PM);
+      const uint32_t gb = (ok && gi == 1 ? 1u : 0u) | (ok && gi == nx - 2 ? 2u : 0u) |
+                          (ok && gj == 1 ? 4u : 0u) | (ok && gj == ny - 2 ? 8u : 0u);
+      gmask |= gb << (4 * (c * 2 + PM));
+    }
+
+  auto slot = [](int m) { return m & (NP - 1); };
+  auto plane_ok = [&](int m) { return m >= zlo && m < zhi; };
+  auto stage_on = [&](int c, int m) {
+    const int h = NC - 1 - c;
+    return m >= z0 - h && m < z1 + h && m >= ulo && m < uhi;
+  };
+
+  struct PRec {
+    Coefs<T> q;
+    T b;
+  };
+
+  // the body, with the z-reflection (the last chunk of a single-launch rank-slab sweep) a
+  // compile-time property: no per-difference selects in the common case
+  auto run = [&](auto flip_c) {
+    constexpr bool FLIP = decltype(flip_c)::value;
+    T up[4];
+    T tn[4][4][RS];  // tensor of plane k, buffer (k - kbeg) & 3, per point
+    T bn[4][4];      // b of that plane
+    PRec rec[4][4];  // records waiting for their stage, buffer (plane - kbeg) & 3
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        rec[q][s].q = Coefs<T>{};
+        rec[q][s].b = T(0);
+      }
+
+    auto load_u = [&](int m) {
+      m = min(max(m, zlo), zhi - 1);
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) up[s] = buf_load<T>(rs, usrc[s], 0u);
+    };
+    auto put_u = [&](int m) {
+      T* P = ring + slot(m) * PLANE;
+      if (has) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) P[uofs(s)] = up[s];
+      }
+    };
+    auto load_t = [&](int m, T (&t)[4][RS], T (&bb)[4]) {
+#ifdef MAD_PG_NO_T  // measurement builds only: no tensor / b stream
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int q = 0; q < RS; ++q) t[s][q] = T(0.01 * (q + 1) + 0.001 * m);
+        bb[s] = T(0.5);
+      }
+      return;
+#endif
+      m = min(max(m, zlo), zhi - 1);
+      const __amdgpu_buffer_rsrc_t rt = buf_rsrc(ct + (int64_t)m * sz * RS);
+      const __amdgpu_buffer_rsrc_t rb = buf_rsrc(b + (int64_t)m * sz);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        buf_load_rec<T, RS>(rt, tof[s], t[s]);
+        bb[s] = buf_load<T>(rb, usrc[s], 0u);
+      }
+    };
+    // exchange plane <- a_x a_y e_xy e_xz e_yz of this thread's four points
+    auto put_x = [&](const T (&t)[4][RS]) {
+      if (has) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          T* P = xb + uofs(s);
+          P[0 * XPLANE] = t[s][0];
+          P[1 * XPLANE] = t[s][1];
+          P[2 * XPLANE] = t[s][3];
+          P[3 * XPLANE] = t[s][4];
+          P[4 * XPLANE] = t[s][5];
+        }
+      }
+    };
+    // records of plane k: g from the exchange plane (x/y) and the z neighbours' tensors
+    auto make_rec = [&](int k, const T (&tc)[4][RS], const T (&bc)[4], const T (&tm)[4][RS],
+                        const T (&tp)[4][RS], PRec (&out)[4]) {
+#pragma clang fp contract(off)
+      // fast path: central differences in x/y (the block's own neighbours from registers,
+      // the others from the exchange plane) and z (physical +z minus -z), g per point
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ox = s & 1, oy = s >> 1;
+        const T* X = xb + uofs(s);
+#ifndef MAD_PG_NO_X
+        auto xp = [&](int C, int XC) { return ox == 0 ? tc[s + 1][C] : X[XC * XPLANE + 1 - HALF]; };
+        auto xm = [&](int C, int XC) { return ox == 1 ? tc[s - 1][C] : X[XC * XPLANE + HALF - 1]; };
+        auto yp = [&](int C, int XC) { return oy == 0 ? tc[s + 2][C] : X[XC * XPLANE + PITCH]; };
+        auto ym = [&](int C, int XC) { return oy == 1 ? tc[s - 2][C] : X[XC * XPLANE - PITCH]; };
+#else  // measurement builds only: in-plane differences from registers only
+        (void)X;
+        (void)ox;
+        (void)oy;
+        auto xp = [&](int C, int) { return tc[s ^ 1][C]; };
+        auto xm = [&](int C, int) { return tc[s][C]; };
+        auto yp = [&](int C, int) { return tc[s ^ 2][C]; };
+        auto ym = [&](int C, int) { return tc[s][C]; };
+#endif
+        const T dxax = xp(0, 0) - xm(0, 0);
+        const T dyay = yp(1, 1) - ym(1, 1);
+        const T dxexy = xp(3, 2) - xm(3, 2);
+        const T dyexy = yp(3, 2) - ym(3, 2);
+        const T dxexz = xp(4, 3) - xm(4, 3);
+        const T dyeyz = yp(5, 4) - ym(5, 4);
+        const T dzaz = FLIP ? tm[s][2] - tp[s][2] : tp[s][2] - tm[s][2];
+        const T dzexz = FLIP ? tm[s][4] - tp[s][4] : tp[s][4] - tm[s][4];
+        const T dzeyz = FLIP ? tm[s][5] - tp[s][5] : tp[s][5] - tm[s][5];
+        PRec& R = out[s];
+        R.q.ax = tc[s][0];
+        R.q.ay = tc[s][1];
+        R.q.az = tc[s][2];
+        R.q.exy = tc[s][3];
+        R.q.exz = tc[s][4];
+        R.q.eyz = tc[s][5];
+        g_combine<T, 3, KFULL>(dxax, dyay, dzaz, dxexy, dyexy, dxexz, dzexz, dyeyz, dzeyz, R.q.gx,
+                               R.q.gy, R.q.gz);
+        R.b = bc[s];
+      }
+      // domain faces (x/y: tiles touching a face; z: two planes per sweep): g of the
+      // flagged points again, with the reference's one-sided second-order differences
+      // (x/y: rows / half-rows +-2 away in the exchange plane; z: the planes two away,
+      // reloaded -- their buffers are gone or not yet filled)
+      const bool lb = k == 0 && !zlo_g, hb = k == g.nz - 1 && !zhi_g;
+#ifdef MAD_PG_NO_FACE  // measurement builds only: no face corrections (wrong at faces)
+      if (false) {
+#else
+      if (bflags != 0u || lb || hb) {
+#endif
+        const bool zlo_f = FLIP ? hb : lb, zhi_f = FLIP ? lb : hb;  // physical z faces
+        const __amdgpu_buffer_rsrc_t rm = buf_rsrc(ct + (int64_t)max(k - 2, zlo) * sz * RS);
+        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(ct + (int64_t)min(k + 2, zhi - 1) * sz * RS);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t bf = (bflags >> (4 * s)) & 15u;
+          if (!bf && !lb && !hb) continue;
+          const int ox = s & 1, oy = s >> 1;
+          const T* X = xb + uofs(s);
+          const bool xl = bf & 1u, xh = bf & 2u, yl = bf & 4u, yh = bf & 8u;
+          auto xp = [&](int C, int XC) { return ox == 0 ? tc[s + 1][C] : X[XC * XPLANE + 1 - HALF]; };
+          auto xm = [&](int C, int XC) { return ox == 1 ? tc[s - 1][C] : X[XC * XPLANE + HALF - 1]; };
+          auto yp = [&](int C, int XC) { return oy == 0 ? tc[s + 2][C] : X[XC * XPLANE + PITCH]; };
+          auto ym = [&](int C, int XC) { return oy == 1 ? tc[s - 2][C] : X[XC * XPLANE - PITCH]; };
+          auto dx = [&](int C, int XC) {
+            return gdelta(X[XC * XPLANE - 1], xm(C, XC), tc[s][C], xp(C, XC), X[XC * XPLANE + 1], xl, xh);
+          };
+          auto dy = [&](int C, int XC) {
+            return gdelta(X[XC * XPLANE - 2 * PITCH], ym(C, XC), tc[s][C], yp(C, XC),
+                          X[XC * XPLANE + 2 * PITCH], yl, yh);
+          };
+          auto dz = [&](int C) {
+            T lm2 = T(0), lp2 = T(0);
+            if (lb || hb) {
+              lm2 = buf_load<T>(rm, tof[s], C * TS);
+              lp2 = buf_load<T>(rp, tof[s], C * TS);
+            }
+            const T lm1 = tm[s][C], lp1 = tp[s][C];
+            // logical k-2, k-1, k+1, k+2 -> physical -2, -1, +1, +2
+            return FLIP ? gdelta(lp2, lp1, tc[s][C], lm1, lm2, zlo_f, zhi_f)
+                        : gdelta(lm2, lm1, tc[s][C], lp1, lp2, zlo_f, zhi_f);
+          };
+          PRec& R = out[s];
+          g_combine<T, 3, KFULL>(dx(0, 0), dy(1, 1), dz(2), dx(3, 2), dy(3, 2), dx(4, 3), dz(4), dy(5, 4),
+                                 dz(5), R.q.gx, R.q.gy, R.q.gz);
+        }
+      }
+    };
+    auto stage = [&](int c, int k, int PM, const PRec (&rq)[4]) {
+      const int m = k - c;
+      if (!stage_on(c, m)) return;
+#ifdef MAD_PG_NO_STAGE  // measurement builds only: no stage reads / arithmetic
+      if (c >= 0) {
+        const int s0 = ((c & 1) ^ PM) + 2 * (((c >> 1) & 1) ^ PM);
+        if ((vmask >> (c * 2 + PM)) & 1u) ring[slot(m) * PLANE + uofs(s0)] = rq[s0].q.gx + rq[s0].b;
+        return;
+      }
+#endif
+      const int ox = (c & 1) ^ PM, oy = ((c >> 1) & 1) ^ PM, s = ox + 2 * oy;
+      const int zm = (m == 0 && !zlo_g) ? 1 : m - 1;
+      const int zp = (m == g.nz - 1 && !zhi_g) ? g.nz - 2 : m + 1;
+      T* A0 = ring + slot(m) * PLANE + uofs(s);
+      // physical -z / +z neighbour planes (swapped in the reflected view)
+      const T* Am = ring + slot(FLIP ? zp : zm) * PLANE + uofs(s);
+      const T* Ap = ring + slot(FLIP ? zm : zp) * PLANE + uofs(s);
+      const int ox_p = ox ? 1 - HALF : HALF;
+      const int ox_m = ox ? -HALF : HALF - 1;
+      T nb[18];
+      nb[0] = A0[ox_p];
+      nb[1] = A0[ox_m];
+      nb[2] = A0[PITCH];
+      nb[3] = A0[-PITCH];
+      nb[4] = Ap[0];
+      nb[5] = Am[0];
+      nb[6] = A0[ox_p + PITCH];
+      nb[7] = A0[ox_p - PITCH];
+      nb[8] = A0[ox_m + PITCH];
+      nb[9] = A0[ox_m - PITCH];
+      nb[10] = Ap[ox_p];
+      nb[11] = Am[ox_p];
+      nb[12] = Ap[ox_m];
+      nb[13] = Am[ox_m];
+      nb[14] = Ap[PITCH];
+      nb[15] = Am[PITCH];
+      nb[16] = Ap[-PITCH];
+      nb[17] = Am[-PITCH];
+      T D, S;
+      stencil_combine<T, 3, KFULL>(rq[s].q, nb, D, S);
+      const T v = gs_update(rq[s].b, S, D);
+      const int bit = c * 2 + PM;
+      if ((vmask >> bit) & 1u) *A0 = v;
+#ifdef MAD_PG_NO_FACE
+      if (false) {
+#else
+      if (!interior) {
+#endif
+        const uint32_t gb = (gmask >> (4 * bit)) & 15u;
+        if (gb) {
+          // mirror images u~(-1) = u(1), u~(n) = u(n-2): same row parity, +-1 in the half
+          // row (x) and +-2 rows (y); corners need both (gb is 0 for invalid points)
+          const int xs[3] = {0, (gb & 1u) ? -1 : 0, (gb & 2u) ? 1 : 0};
+          const int ys[3] = {0, (gb & 4u) ? -2 * PITCH : 0, (gb & 8u) ? 2 * PITCH : 0};
+#pragma unroll
+          for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int bq = 0; bq < 3; ++bq) {
+              if ((a == 0 && bq == 0) || (a > 0 && xs[a] == 0) || (bq > 0 && ys[bq] == 0)) continue;
+              A0[xs[a] + ys[bq]] = v;
+            }
+        }
+      }
+    };
+
+    // prologue: u planes kbeg-1, kbeg in the ring, kbeg+1 in registers; tensors of planes
+    // kbeg-1 .. kbeg+1 in buffers 3, 0, 1
+    for (int m = kbeg - 1; m <= kbeg; ++m)
+      if (plane_ok(m)) {
+        load_u(m);
+        put_u(m);
+      }
+    load_u(kbeg + 1);
+    load_t(kbeg - 1, tn[3], bn[3]);
+    load_t(kbeg, tn[0], bn[0]);
+    load_t(kbeg + 1, tn[1], bn[1]);
+
+    // Whole groups of 4 steps: a step past kend runs no stage and stores nothing (stage_on,
+    // the output range), and an unconditional body keeps the records' live ranges to their
+    // real uses (a guarded step would keep every pending record alive across its join).
+    // Barriers: one after the plane / exchange writes, one after each of stages 0-2.  None
+    // after stage 3: the next step writes ring slot k+3 (8 slots, nobody reads it) and the
+    // exchange plane (last read before stage 0), and a thread's stores read only its own
+    // points.
+    for (int k0 = kbeg; k0 <= kend; k0 += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u;
+        asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(bflags), "+v"(omask));
+        if (plane_ok(k + 1)) put_u(k + 1);
+        put_x(tn[u]);
+        load_u(k + 2);
+        __syncthreads();
+        make_rec(k, tn[u], bn[u], tn[(u + 3) & 3], tn[(u + 1) & 3], rec[u]);
+        // plane k+2's tensor: issued once g of plane k is formed (plane k's tensor now
+        // lives on in the records), in flight through this step's stages
+        load_t(k + 2, tn[(u + 2) & 3], bn[(u + 2) & 3]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          stage(c, k, (u ^ c) & 1, rec[(u - c) & 3]);
+          if (c < NC - 1) __syncthreads();
+        }
+        const int mo = k - NC + 1;
+        if (mo >= z0 && mo < z1) {
+          const T* P = ring + slot(mo) * PLANE;
+          const __amdgpu_buffer_rsrc_t ro = buf_rsrc(uout + (int64_t)mo * sz);
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#ifndef MAD_PG_NO_STORE  // measurement builds only: no output stores
+            if ((omask >> s) & 1u) buf_store<T>(P[uofs(s)], ro, usrc[s]);
+#else
+            if ((omask >> s) & 1u && P[uofs(s)] == T(-12345.678)) buf_store<T>(P[uofs(s)], ro, usrc[s]);
+#endif
+          if (signals && mo == GHOST - 1) {
+            __threadfence();
+            __syncthreads();
+            if (tid == 0)
+              __hip_atomic_fetch_add(sig + (FLIP ? 1 : 0), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+      }
+    }
+  };
+  if (flip)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
+}
+
+// tensor records (a_x a_y a_z e_xy e_xz e_yz) of the full 3D operator from its coefficient
+// records (fields 0-2 and 6-8), plane range [p0, p1) (ghost planes included)
+template <typename T>
+__global__ void __launch_bounds__(256) pack_tensor_k(const T* __restrict__ cf, T* __restrict__ ct,
+                                                     int64_t sz, int rs, int p0, int64_t n) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = (int64_t)p0 * sz + q;
+    const T* s = cf + p * rs;
+    T* d = ct + p * 6;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+    d[3] = s[6];
+    d[4] = s[7];
+    d[5] = s[8];
   }
 }
 
@@ -1989,6 +2464,100 @@ __global__ void __launch_bounds__(256) build_coef3_k(const double* __restrict__ 
       zp[d] = k + 2 < nz ? Mz[d][col + (int64_t)(k + 2) * sz] : 0.0;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// g from the stored (storage-type) a / e coefficients.  With a_d = dt M_dd / h_d^2 and
+// e_dd2 = dt M_dd2 / (2 h_d h_d2) the reference's g_d = dt/(2h_d) sum_d2 delta_d2 M_d,d2
+// / (2 h_d2) (GH.hxx:447-474) is, exactly,
+//   g_x = 1/4 delta_x a_x + 1/2 delta_y e_xy + 1/2 delta_z e_xz   (and cyclically)
+// with delta the reference's 2h-scaled differences (central; one-sided second order at
+// the border, delta_f).  Every kernel evaluates g through these helpers on the same
+// T-typed inputs in the same order, so a g recomputed inside a sweep (gs_fusedg_k) is
+// bit-identical to the g build_g_k stores for the per-point kernels.
+template <typename T>
+__device__ __forceinline__ T gdelta(T fm2, T fm1, T f0, T fp1, T fp2, bool lo, bool hi) {
+#pragma clang fp contract(off)
+  if (lo) {
+    T t = T(-3) * f0;
+    t = t + T(4) * fp1;
+    return t - fp2;
+  }
+  if (hi) {
+    T t = T(3) * f0;
+    t = t - T(4) * fm1;
+    return t + fm2;
+  }
+  return fp1 - fm1;
+}
+
+// g_d from the differences of the coefficient fields (dA_d2 = delta_d2 of field A)
+template <typename T, int DIM, int KIND>
+__device__ __forceinline__ void g_combine(T dxax, T dyay, T dzaz, T dxexy, T dyexy, T dxexz,
+                                          T dzexz, T dyeyz, T dzeyz, T& gx, T& gy, T& gz) {
+#pragma clang fp contract(off)
+  if (KIND == KFULL) {
+    gx = T(0.25) * dxax + T(0.5) * dyexy;
+    gy = T(0.5) * dxexy + T(0.25) * dyay;
+    if (DIM == 3) {
+      gx = gx + T(0.5) * dzexz;
+      gy = gy + T(0.5) * dzeyz;
+      gz = (T(0.5) * dxexz + T(0.5) * dyeyz) + T(0.25) * dzaz;
+    } else {
+      gz = T(0);
+    }
+  } else {
+    gx = T(0.25) * dxax;
+    gy = T(0.25) * dyay;
+    gz = (DIM == 3) ? T(0.25) * dzaz : T(0);
+  }
+}
+
+// stored g of one level (global grid, records already holding a / e): per point, the
+// neighbours' coefficients from memory.  In place: g slots are written, a / e only read.
+template <typename T, int DIM, int KIND>
+__global__ void __launch_bounds__(256) build_g_k(T* __restrict__ cf, int nx, int ny, int nz, int rs,
+                                                 Rat<T> rat) {
+  using L = CoefLayout<DIM, KIND>;
+  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nx || j >= ny) return;
+  const int hx0 = (nx + 1) / 2;
+  auto Q = [&](int ii, int jj, int kk) {
+    ii = min(max(ii, 0), nx - 1);
+    jj = min(max(jj, 0), ny - 1);
+    kk = min(max(kk, 0), nz - 1);
+    const int64_t c = ((int64_t)kk * ny + jj) * nx + ((ii & 1) ? hx0 + (ii >> 1) : (ii >> 1));
+    Coefs<T> q;
+    load_coefs<T, DIM, KIND>(cf, c, rs, rat, q);
+    return q;
+  };
+  const bool xl = i == 0, xh = !xl && i == nx - 1;
+  const bool yl = j == 0, yh = !yl && j == ny - 1;
+  const bool zl = k == 0, zh = !zl && k == nz - 1;
+  const Coefs<T> c0 = Q(i, j, k);
+  const Coefs<T> xm1 = Q(i - 1, j, k), xp1 = Q(i + 1, j, k), xm2 = Q(i - 2, j, k), xp2 = Q(i + 2, j, k);
+  const Coefs<T> ym1 = Q(i, j - 1, k), yp1 = Q(i, j + 1, k), ym2 = Q(i, j - 2, k), yp2 = Q(i, j + 2, k);
+  T dxax = gdelta(xm2.ax, xm1.ax, c0.ax, xp1.ax, xp2.ax, xl, xh);
+  T dyay = gdelta(ym2.ay, ym1.ay, c0.ay, yp1.ay, yp2.ay, yl, yh);
+  T dxexy = gdelta(xm2.exy, xm1.exy, c0.exy, xp1.exy, xp2.exy, xl, xh);
+  T dyexy = gdelta(ym2.exy, ym1.exy, c0.exy, yp1.exy, yp2.exy, yl, yh);
+  T dxexz = gdelta(xm2.exz, xm1.exz, c0.exz, xp1.exz, xp2.exz, xl, xh);
+  T dyeyz = gdelta(ym2.eyz, ym1.eyz, c0.eyz, yp1.eyz, yp2.eyz, yl, yh);
+  T dzaz = T(0), dzexz = T(0), dzeyz = T(0);
+  if (DIM == 3) {
+    const Coefs<T> zm1 = Q(i, j, k - 1), zp1 = Q(i, j, k + 1), zm2 = Q(i, j, k - 2), zp2 = Q(i, j, k + 2);
+    dzaz = gdelta(zm2.az, zm1.az, c0.az, zp1.az, zp2.az, zl, zh);
+    dzexz = gdelta(zm2.exz, zm1.exz, c0.exz, zp1.exz, zp2.exz, zl, zh);
+    dzeyz = gdelta(zm2.eyz, zm1.eyz, c0.eyz, zp1.eyz, zp2.eyz, zl, zh);
+  }
+  T gx, gy, gz;
+  g_combine<T, DIM, KIND>(dxax, dyay, dzaz, dxexy, dyexy, dxexz, dzexz, dyeyz, dzeyz, gx, gy, gz);
+  const int64_t o = (((int64_t)k * ny + j) * nx + ((i & 1) ? hx0 + (i >> 1) : (i >> 1))) * rs;
+  cf[o + L::NA] = gx;
+  cf[o + L::NA + 1] = gy;
+  if (DIM == 3) cf[o + L::NA + 2] = gz;
 }
 
 // ---------------------------------------------------------------------------

@@ -257,6 +257,10 @@ struct LevelData {
   T* t = nullptr;  // WJ ping-pong / scratch
   T* cf = nullptr;        // field 0, plane 0 (ghost planes precede it on rank slabs)
   T* cf_alloc = nullptr;
+  // full 3D tensor records [a_x a_y a_z e_xy e_xz e_yz] (same point order and ghost planes
+  // as cf, no g): the fused sweep gs_fusedg_k reads these and recomputes g
+  T* ct = nullptr;
+  T* ct_alloc = nullptr;
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -343,7 +347,10 @@ class Solver final : public SolverBase {
       // scatter of b into the 40-B records (partial-line writes, 512^3) costs more than
       // it saves (VED diffusion 126 -> 116.5 ms without it, profiles/r01_brec_ab.log).
       // MAD_BREC=0/1 overrides (A/B runs).
-      bool brec_on = c->d.cycle == MAD_SMOOTHER;
+      // The full-tensor GS sweep (gs_fusedg_k) reads the dense b with its plane stream, so
+      // it needs no record b.
+      bool brec_on = c->d.cycle == MAD_SMOOTHER &&
+                     !(c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d));
       if (const char* e = std::getenv("MAD_BREC")) brec_on = e[0] != '0';
       L.brec = (dim == 3 && l == 0 && brec_on);
       L.g.rs = ncoef_ + (L.brec ? 1 : 0);
@@ -354,6 +361,13 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * ctot));
       HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
+      if (dim == 3 && c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d)) {
+        const int64_t tplane = L.g.sz * 6;
+        const int64_t ttot = (L.g.nz + 2 * cgp) * tplane + 2 * margin * 6;
+        HIP_CHECK(hipMalloc(&L.ct_alloc, sizeof(T) * ttot));
+        HIP_CHECK(hipMemsetAsync(L.ct_alloc, 0, sizeof(T) * ttot, c->stream));
+        L.ct = L.ct_alloc + margin * 6 + cgp * tplane;
+      }
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
@@ -371,7 +385,7 @@ class Solver final : public SolverBase {
         // than a whole 64-plane rank sweep -- while an event after the short boundary
         // launch releases the exchange within ~0.05 ms, so boundary + interior
         // launches (parts 1, 2) win.
-        if (can_wait && c->d.gs_kernel == 4) {
+        if (can_wait && (c->d.gs_kernel == 4 || c->d.gs_kernel == 6)) {
           HIP_CHECK(hipExtMallocWithFlags((void**)&lv_[l].sig, 2 * sizeof(uint32_t),
                                           hipMallocSignalMemory));
           const uint32_t zero[2] = {0u, 0u};
@@ -487,7 +501,7 @@ class Solver final : public SolverBase {
   static int64_t margin_elems(const Geo& g) { return 48 * g.sy + 512; }
 
   bool use_fused(int l) const {
-    const int v = c_->d.gs_kernel;  // 0 auto (v3), 1 per-colour passes, 2 fused v2, 3 / 4 fused v3
+    const int v = c_->d.gs_kernel;  // 0 auto (v3), 1 per-colour passes, 2 fused v2, 3 / 4 fused v3, 5 / 6 fused g-free
     if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL) return false;
     if (v == 1) return false;
     if (v >= 2) return true;
@@ -539,13 +553,104 @@ class Solver final : public SolverBase {
   // 3 whole slab with the last chunk marched downward and the edge-plane signals
   // (single-launch rank-slab sweep); gs_kernel 4 runs part 0 with the downward last
   // chunk (no signals)
+  // full-tensor sweeps with g recomputed in-kernel (gs_fusedg_k, tensor records L.ct):
+  // gs_kernel 5 / 6, or MAD_FUSEDG=1 for the fused forms 0 / 3 / 4 (A/B runs).  Not the
+  // default: it moves the 36 algorithmic bytes instead of 48, but its pending records
+  // (~250 VGPRs per thread) leave 2 waves per SIMD and it runs latency-bound
+  static bool fusedg_env() {
+    static const bool v = [] {
+      const char* e = std::getenv("MAD_FUSEDG");
+      return e && e[0] == '1';
+    }();
+    return v;
+  }
+  static bool fusedg_wanted(const mad_desc& d) {
+    return d.gs_kernel == 5 || d.gs_kernel == 6 ||
+           (fusedg_env() && (d.gs_kernel == 0 || d.gs_kernel == 3 || d.gs_kernel == 4));
+  }
+  bool fusedg_on(const LevelData<T>& L) const {
+    return L.ct != nullptr && c_->kind == KFULL && fusedg_wanted(c_->d);
+  }
+  // gs_fusedg_k tile: fp32 64x16 (432 blocks of 2x2 points, 512 threads, 2 waves per
+  // SIMD for ~200 VGPRs of records in flight), 32x32 (MAD_FUSEDG_TILE=1) or 32x16 on 256
+  // threads, two workgroups per CU (MAD_FUSEDG_TILE=2); fp64 32x16 on 256 threads (one wave
+  // per SIMD)
+  static int fusedg_tile() {
+    static const int v = [] {
+      const char* e = std::getenv("MAD_FUSEDG_TILE");
+      return e ? std::atoi(e) : 0;
+    }();
+    return v;
+  }
+  void fusedg_dims(int* tx, int* ty, int* nt) const {
+    if (sizeof(T) == 8) {
+      *tx = 32; *ty = 16; *nt = 256;
+    } else if (fusedg_tile() == 1) {
+      *tx = 32; *ty = 32; *nt = 512;
+    } else if (fusedg_tile() == 2) {
+      *tx = 32; *ty = 16; *nt = 256;
+    } else {
+      *tx = 64; *ty = 16; *nt = 512;
+    }
+  }
+
+  // z-chunks of one launch of `part` (see launch_fused) over `tiles` tiles per plane
+  ZRange part_range(LevelData<T>& L, int tiles, const FusedCfg& fc, int part, int* flip,
+                    uint32_t** sig) {
+    const int nz = L.g.nz;
+    ZRange zr = whole_range(nz, tiles, fc);
+    *flip = ((c_->d.gs_kernel == 4 || c_->d.gs_kernel == 6) && part == 0) ? 1 : 0;
+    *sig = nullptr;
+    if (part == 3) {
+      REQUIRE(zr.nchunks >= 2 && zr.zc >= GHOST, MAD_ERR_UNSUPPORTED, "slab too thin for the single-launch sweep");
+      *flip = 1;
+      *sig = L.sig;
+    } else if (part == 1) {
+      zr = ZRange{0, boundary_planes(), nz - boundary_planes(), 2};
+    } else if (part == 2) {
+      const int ni = nz - 2 * boundary_planes();
+      static const int iblocks = [&] {
+        const char* e = std::getenv("MAD_INTERIOR_BLOCKS");  // tuning runs only
+        return e ? std::max(1, std::atoi(e)) : fc.blocks;
+      }();
+      int chunks = std::max(1, std::min((iblocks + tiles - 1) / tiles, std::max(1, ni / 16)));
+      const int zc = (ni + chunks - 1) / chunks;
+      zr = ZRange{boundary_planes(), zc, zc, (ni + zc - 1) / zc};
+    }
+    return zr;
+  }
+
+  template <int TX, int TY, int NT, int MINW = NT / 256>
+  void launch_fusedg(LevelData<T>& L, int part) {
+    const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
+    const int tiles = ntx * nty;
+    FusedCfg fc;
+    fc.blocks = 256 * (MINW * 256 / NT);  // one round of the workgroups a CU holds
+    if (const char* e = std::getenv("MAD_FUSED_BLOCKS")) fc.blocks = std::max(1, std::atoi(e));
+    int flip = 0;
+    uint32_t* sig = nullptr;
+    const ZRange zr = part_range(L, tiles, fc, part, &flip, &sig);
+    using FG = FusedGGeom<TX, TY>;
+    constexpr size_t lds = sizeof(T) * FG::ELEMS;
+    static_assert(lds <= 160 * 1024, "gs_fusedg_k tile exceeds the LDS");
+    auto kern = gs_fusedg_k<T, TX, TY, NT, MINW>;
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr = true;
+    }
+    REQUIRE(L.g.nx >= 3 && L.g.ny >= 3 && L.g.nz >= 3, MAD_ERR_UNSUPPORTED, "fused sweep needs >= 3 points per axis");
+    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * zr.nchunks)), dim3(NT), lds, c_->stream, L.x, L.t, L.b,
+                       L.ct, L.g, zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig);
+  }
+
   template <int KD, int TX, int TY, int NT>
   void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
     const int nz = L.g.nz;
     ZRange zr = whole_range(nz, tiles, fc);
-    int flip = (c_->d.gs_kernel == 4 && part == 0) ? 1 : 0;
+    int flip = ((c_->d.gs_kernel == 4 || c_->d.gs_kernel == 6) && part == 0) ? 1 : 0;
     uint32_t* sig = nullptr;
     if (part == 3) {
       zr = whole_range(nz, tiles, fc);
@@ -602,6 +707,16 @@ class Solver final : public SolverBase {
 
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
   void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {
+    if (fusedg_on(L)) {
+      int tx, ty, nt;
+      fusedg_dims(&tx, &ty, &nt);
+      FusedCfg fc;
+      fc.blocks = (sizeof(T) == 4 && fusedg_tile() == 2) ? 512 : 256;
+      if (const char* e = std::getenv("MAD_FUSED_BLOCKS")) fc.blocks = std::max(1, std::atoi(e));
+      *tiles = ((L.g.nx + tx - 1) / tx) * ((L.g.ny + ty - 1) / ty);
+      *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
+      return;
+    }
     const FusedCfg& fc = fused_cfg();
     int tx = 64, ty = 16;
     if (c_->kind == KFULL) {
@@ -615,7 +730,18 @@ class Solver final : public SolverBase {
 
   void launch_fused_part(LevelData<T>& L, int part) {
     const FusedCfg& fc = fused_cfg();
-    if (c_->kind == KFULL) {
+    if (fusedg_on(L)) {
+      if constexpr (sizeof(T) == 8) {
+        launch_fusedg<32, 16, 256>(L, part);
+      } else {
+        if (fusedg_tile() == 1)
+          launch_fusedg<32, 32, 512>(L, part);
+        else if (fusedg_tile() == 2)
+          launch_fusedg<32, 16, 256, 2>(L, part);
+        else
+          launch_fusedg<64, 16, 512>(L, part);
+      }
+    } else if (c_->kind == KFULL) {
       if (fc.tile == 1)
         launch_fused<KFULL, 64, 32, 1024>(L, fc, part);
       else if (fc.tile == 2)
@@ -651,6 +777,19 @@ class Solver final : public SolverBase {
     } else if (c_->d.gs_kernel == 2) {
       std::snprintf(buf, sizeof buf, "gs_fused_k<%s, %d, 64, 16, %d, %d>", tn, kind,
                     kind == KFULL ? 512 : 1024, sizeof(T) == 8 ? 2 : 4);
+    } else if (fusedg_on(lv_[l])) {
+      int tx, ty, nt;
+      fusedg_dims(&tx, &ty, &nt);
+      std::snprintf(buf, sizeof buf, "gs_fusedg_k<%s, %d, %d, %d%s>", tn, tx, ty, nt,
+                    (sizeof(T) == 4 && fusedg_tile() == 2) ? ", 2" : "");
+      const LevelData<T>& L = lv_[l];
+      if (c_->comm.active() && c_->geom[l].distributed && L.g.nz >= 3 * boundary_planes()) {
+        int tiles = 0, nchunks = 0;
+        fused_shape(L, &tiles, &nchunks);
+        const bool single = L.sig && nchunks >= 2;
+        return std::string(buf) + (single ? " [rank slab: single launch, edge signals]"
+                                          : " [rank slab: boundary + interior launches]");
+      }
     } else {
       const FusedCfg& fc = fused_cfg();
       int tx = 64, ty = 16, nt = kind == KFULL ? 512 : 1024;
@@ -709,7 +848,7 @@ class Solver final : public SolverBase {
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
-    if (L.brec && c_->d.gs_kernel != 2) {
+    if (L.brec && c_->d.gs_kernel != 2 && !fusedg_on(L)) {
       sync_brec(l);
     } else if (!L.b_halo_ok) {
       halo(l, L.b, GHOST);
@@ -1143,7 +1282,7 @@ class Solver final : public SolverBase {
       const char* e = std::getenv("MAD_VGRAPH_RANKS");
       return !(e && e[0] == '0');
     }();
-    return env_ok && c_->comm.mode() == Comm::RCCL && c_->d.gs_kernel != 4;
+    return env_ok && c_->comm.mode() == Comm::RCCL && c_->d.gs_kernel != 4 && c_->d.gs_kernel != 6;
   }
 
   struct HaloFlags {
@@ -1526,6 +1665,7 @@ class Solver final : public SolverBase {
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
+      if (L.ct_alloc) (void)hipFree(L.ct_alloc);
     }
     lv_.clear();
     if (part_) (void)hipFree(part_);
@@ -1637,6 +1777,13 @@ class Solver final : public SolverBase {
         });
       }
       HIP_CHECK(hipGetLastError());
+      // g from the stored a / e (build_g_k): the one definition every kernel shares,
+      // including the sweeps that recompute g in-kernel instead of reading it
+      dispatch(dim, c_->kind, [&](auto D, auto K) {
+        hipLaunchKernelGGL((build_g_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, dst,
+                           (int)G.n[0], (int)G.n[1], (int)G.n[2], L.g.rs, L.rat);
+      });
+      HIP_CHECK(hipGetLastError());
       if (slab) {
         // owned planes plus up to GHOST neighbour planes on each side (whole plane blocks)
         const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
@@ -1648,6 +1795,15 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipStreamSynchronize(c_->stream));
         HIP_CHECK(hipFree(full_cf));
         full_cf = nullptr;
+      }
+      if (L.ct) {
+        // tensor records of every allocated plane the coefficient records hold
+        const int p0 = L.g.zlo_ghost ? -GHOST : 0;
+        const int p1 = L.g.nz + (L.g.zhi_ghost ? GHOST : 0);
+        const int64_t n = (int64_t)(p1 - p0) * L.g.sz;
+        hipLaunchKernelGGL((pack_tensor_k<T>), dim3(flat_blocks(n)), dim3(256), 0, c_->stream, L.cf,
+                           L.ct, L.g.sz, L.g.rs, p0, n);
+        HIP_CHECK(hipGetLastError());
       }
       if (l == nl - 1) build_coarsest_matrix(fine);
     }
