@@ -63,7 +63,10 @@ typedef enum mad_dtype {
   MAD_F32 = 6, MAD_F64 = 7
 } mad_dtype;
 
-typedef enum mad_precision { MAD_FP32 = 0, MAD_FP64 = 1 } mad_precision;
+/* MAD_FP32_REFINE: fp32 hierarchy (storage + arithmetic) inside a mixed-precision defect
+   correction -- level 0's iterate, rhs and residual in fp64 with the fp64 operator, one fp32
+   cycle per correction -- so a solve reaches the reference's fp64 tolerances (1e-10) */
+typedef enum mad_precision { MAD_FP32 = 0, MAD_FP64 = 1, MAD_FP32_REFINE = 2 } mad_precision;
 
 typedef enum mad_tensor_kind {
   MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */
@@ -92,7 +95,8 @@ typedef struct mad_desc {
   double tolerance;              /* SetTolerance,          default 1e-6 */
   double omega;                  /* WJ weight (MultigridWeightedJacobiSmoother ctor), default 2/3 */
   int32_t verbose;               /* SetVerbose,            default 0 */
-  int32_t precision;             /* MAD_FP32 (default) or MAD_FP64 storage + arithmetic */
+  int32_t precision;             /* MAD_FP32 (default), MAD_FP64 storage + arithmetic, or
+                                    MAD_FP32_REFINE (fp32 cycles, fp64 defect correction) */
   int32_t stall_guard;           /* 1: end a time step once relres stops improving (the fp32
                                     floor); default 1 for FP32, 0 for FP64 */
   int32_t device;                /* HIP device ordinal, -1 = current device */

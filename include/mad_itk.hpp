@@ -137,7 +137,7 @@ class MultigridAnisotropicDiffusionImageFilter {
   void SetTolerance(Precision t) { desc_.tolerance = t; }
   void SetVerbose(bool v) { desc_.verbose = v ? 1 : 0; }
   // MI355X execution options (no reference counterpart)
-  void SetPrecision(int32_t p) { desc_.precision = p; desc_.stall_guard = (p == MAD_FP32); }
+  void SetPrecision(int32_t p) { desc_.precision = p; desc_.stall_guard = (p != MAD_FP64); }
   void SetDevice(int32_t d) { desc_.device = d; }
 
   // SetDiffusionTensor (.hxx:66-101): copied and cast to fp64 at call time

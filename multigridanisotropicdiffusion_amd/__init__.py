@@ -6,7 +6,7 @@ ABI in include/mad.h).  This package is the host-side mirror of the reference's
 operator surface; it never falls back to a CPU implementation.
 """
 from . import _capi as capi
-from ._capi import (FMG, FP32, FP64, GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, SMOOTHER, VCYCLE,
+from ._capi import (FMG, FP32, FP32_REFINE, FP64, GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, SMOOTHER, VCYCLE,
                     WEIGHTED_JACOBI, MadError)
 from .filters import (Image, MultigridAnisotropicDiffusionImageFilter,
                       MultigridGaussSeidelLexSmoother, MultigridGaussSeidelSmoother,
@@ -20,5 +20,5 @@ __all__ = [
     "MultigridAnisotropicDiffusionImageFilter", "MultigridGaussSeidelSmoother",
     "MultigridGaussSeidelLexSmoother", "MultigridWeightedJacobiSmoother", "MadError",
     "VCYCLE", "FMG", "SMOOTHER", "GAUSS_SEIDEL", "GAUSS_SEIDEL_LEX", "WEIGHTED_JACOBI",
-    "FP32", "FP64", "VED", "VEDMultigridImageFilter", "mhd",
+    "FP32", "FP32_REFINE", "FP64", "VED", "VEDMultigridImageFilter", "mhd",
 ]

@@ -22,7 +22,7 @@ GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, WEIGHTED_JACOBI = 0, 1, 2
 # mad_dtype
 U8, I8, U16, I16, U32, I32, F32, F64 = range(8)
 # mad_precision
-FP32, FP64 = 0, 1
+FP32, FP64, FP32_REFINE = 0, 1, 2
 # mad_tensor_kind
 TENSOR_AUTO, TENSOR_ISOTROPIC, TENSOR_DIAGONAL, TENSOR_FULL = range(4)
 # mad_which

@@ -2274,6 +2274,15 @@ __global__ void __launch_bounds__(256) convert_k(const S* __restrict__ x, D* __r
     y[q] = (D)x[q];
 }
 
+// defect-correction update u += (double) e (MAD_FP32_REFINE: fp64 iterate, fp32 correction)
+template <typename S>
+__global__ void __launch_bounds__(256) add_conv_k(double* __restrict__ u, const S* __restrict__ e,
+                                                  int64_t n) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x)
+    u[q] += (double)e[q];
+}
+
 // static_cast<OutputPixelType>(double) for integer outputs: truncation toward zero,
 // saturated to the type's range (the reference leaves out-of-range values undefined)
 template <typename S, typename D>

@@ -351,6 +351,7 @@ class Solver final : public SolverBase {
       // it needs no record b.
       bool brec_on = c->d.cycle == MAD_SMOOTHER &&
                      !(c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d));
+      if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
       if (const char* e = std::getenv("MAD_BREC")) brec_on = e[0] != '0';
       L.brec = (dim == 3 && l == 0 && brec_on);
       L.g.rs = ncoef_ + (L.brec ? 1 : 0);
@@ -370,6 +371,26 @@ class Solver final : public SolverBase {
       }
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
+    }
+    refine_ = sizeof(T) == 4 && c->d.precision == MAD_FP32_REFINE;
+    if (refine_) {
+      LevelData<T>& L0 = lv_[0];
+      const int64_t margin = margin_elems(L0.g);
+      const int64_t tot = L0.g.N + 2 * (L0.ghost + margin);
+      for (auto& a : r64alloc_) {
+        HIP_CHECK(hipMalloc(&a, sizeof(double) * tot));
+        HIP_CHECK(hipMemsetAsync(a, 0, sizeof(double) * tot, c->stream));
+      }
+      u64_ = r64alloc_[0] + margin + L0.ghost;
+      b64_ = r64alloc_[1] + margin + L0.ghost;
+      r64_ = r64alloc_[2] + margin + L0.ghost;
+      const int64_t cgp = (dim == 3) ? GHOST : 0;
+      const int64_t cplane = L0.g.sz * ncoef_;
+      const int64_t ctot = (L0.g.nz + 2 * cgp) * cplane + 2 * margin * ncoef_;
+      HIP_CHECK(hipMalloc(&cf64_alloc_, sizeof(double) * ctot));
+      HIP_CHECK(hipMemsetAsync(cf64_alloc_, 0, sizeof(double) * ctot, c->stream));
+      cf64_ = cf64_alloc_ + margin * ncoef_ + cgp * cplane;
+      for (int d = 0; d < 3; ++d) rat64_.r[d] = (c->geom[0].h[0] * c->geom[0].h[0]) / (c->geom[0].h[d] * c->geom[0].h[d]);
     }
     int can_wait = 0;
     if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, c->device) !=
@@ -1000,6 +1021,55 @@ class Solver final : public SolverBase {
 
   double residual(int l, bool want_norm) override { return residual_impl(l, want_norm, true); }
 
+  // fp64 residual of the refined level-0 system: r64 = b64 - A64 u64 (+ ||r||^2 partials),
+  // the reference operator in fp64 (coefficient records cf64_, g from the fp64 tensor)
+  double residual64() {
+    LevelData<T>& L = lv_[0];
+    if (c_->comm.active() && c_->geom[0].distributed) {
+      wait_all_pending();
+      c_->comm.exchange_planes(u64_, L.g.sz, L.g.nz, 1, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(double),
+                               true, c_->stream);
+    }
+    Geo g = L.g;
+    g.rs = ncoef_;
+    int64_t nparts = 0;
+    if (c_->dim == 3 && g.nx >= 16 && g.ny >= 16) {
+      constexpr int TX = 64, TY = 16;
+      const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
+      int chunks = std::max(1, std::min((1024 + ntx * nty - 1) / (ntx * nty), g.nz / 8));
+      const int zc = (g.nz + chunks - 1) / chunks;
+      chunks = (g.nz + zc - 1) / zc;
+      nparts = (int64_t)ntx * nty * chunks;
+      REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
+      auto go = [&](auto K) {
+        constexpr int KD = decltype(K)::value;
+        hipLaunchKernelGGL((resid3_k<double, KD, TX, TY>), dim3((unsigned)nparts), dim3(TX * TY), 0,
+                           c_->stream, u64_, b64_, r64_, cf64_, g, rat64_, zc, ntx, part_);
+      };
+      if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
+      else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
+      else go(std::integral_constant<int, KISO>{});
+    } else {
+      dim3 gr = grid_for(g.nx, g.ny, g.nz, BLK);
+      nparts = (int64_t)gr.x * gr.y * gr.z;
+      REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
+      dispatch(c_->dim, c_->kind, [&](auto D, auto K) {
+        hipLaunchKernelGGL((residual_k<double, D.value, K.value>), gr, BLK, 0, c_->stream, u64_, b64_,
+                           r64_, cf64_, g, rat64_, part_);
+      });
+    }
+    HIP_CHECK(hipGetLastError());
+    return std::sqrt(finish_norm2(nparts, c_->geom[0].distributed));
+  }
+
+  double norm64(const double* a) {
+    const int64_t n = lv_[0].g.N;
+    unsigned nb = flat_blocks(n, 2048);
+    hipLaunchKernelGGL((sumsq_k<double>), dim3(nb), dim3(256), 0, c_->stream, a, n, part_);
+    HIP_CHECK(hipGetLastError());
+    return std::sqrt(finish_norm2(nb, c_->geom[0].distributed));
+  }
+
   // write_r false: only ||r|| is wanted (the per-cycle convergence test), r is not
   // stored (z-marching path; the per-point fallback always stores it)
   double residual_impl(int l, bool want_norm, bool write_r) {
@@ -1440,6 +1510,10 @@ class Solver final : public SolverBase {
   // ------------------------------------------------------------- filter
   void run(const void* in, int in_dtype, void* out, int out_dtype, bool dev_io,
            mad_stats* st) override {
+    if (refine_) {
+      run_refine(in, in_dtype, out, out_dtype, dev_io, st);
+      return;
+    }
     LevelData<T>& L0 = lv_[0];
     const int64_t N = L0.g.N;
     const mad_desc& d = c_->d;
@@ -1522,6 +1596,127 @@ class Solver final : public SolverBase {
     void* dst = out;
     if (!dev_io) dst = scratch_bytes(N * dtype_size(out_dtype));
     convert_out(L0.x, dst, out_dtype, N);
+    if (!dev_io)
+      HIP_CHECK(hipMemcpyAsync(out, dst, N * dtype_size(out_dtype), hipMemcpyDeviceToHost,
+                               c_->stream));
+    HIP_CHECK(hipStreamSynchronize(c_->stream));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    if (st) {
+      std::memset(st, 0, sizeof(*st));
+      st->steps = d.number_of_steps;
+      st->total_cycles = total;
+      st->last_cycles = c_->step_cycles.empty() ? 0 : c_->step_cycles.back();
+      st->stalled = stalled_any ? 1 : 0;
+      st->last_relres = relres;
+      st->setup_ms = c_->setup_ms;
+      st->solve_ms = ms;
+      st->num_levels = (uint32_t)c_->nlev;
+      st->tensor_kind = c_->kind;
+      st->colors = c_->ncolors;
+    }
+  }
+
+  // GenerateData (MAD.hxx:104-297) with mixed-precision defect correction (MAD_FP32_REFINE):
+  // the iterate u and the rhs b of level 0 stay in fp64; every cycle forms the fp64 residual
+  // r = b - A u with the fp64 operator, runs the cycle the CycleType names (one V-cycle, or
+  // one smoother sweep) in fp32 on the error equation A e = r from e = 0, and adds u += e in
+  // fp64.  The fp32 V-cycle only has to reduce the error by its usual factor each time, so
+  // the iteration converges to the fp64 solution (relres to the reference's 1e-10) instead
+  // of stalling at the fp32 floor (~1e-7); relres is the fp64 residual's, as in the
+  // reference's loop (MAD.hxx:207-246).  FMG: the fp32 FMG cycle gives the first iterate.
+  void run_refine(const void* in, int in_dtype, void* out, int out_dtype, bool dev_io,
+                  mad_stats* st) {
+    LevelData<T>& L0 = lv_[0];
+    const int64_t N = L0.g.N;
+    const mad_desc& d = c_->d;
+    const unsigned nb = flat_blocks(N);
+    const void* src = in;
+    if (!dev_io) {
+      void* stage = scratch_bytes(N * dtype_size(in_dtype));
+      HIP_CHECK(hipMemcpyAsync(stage, in, N * dtype_size(in_dtype), hipMemcpyHostToDevice,
+                               c_->stream));
+      src = stage;
+    }
+    convert_to(src, in_dtype, b64_, N, c_->stream);
+    auto to_fp32_rhs = [&](const double* a) {  // level-0 b (fp32) <- a
+      hipLaunchKernelGGL((convert_k<double, T>), dim3(nb), dim3(256), 0, c_->stream, a, L0.b, N);
+      HIP_CHECK(hipGetLastError());
+      L0.b_halo_ok = L0.brec_ok = false;
+    };
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventRecord(e0, c_->stream));
+    c_->step_cycles.clear();
+    c_->step_relres.clear();
+    bool stalled_any = false;
+    unsigned total = 0;
+    double relres = 0.0;
+    for (unsigned step = 0; step < d.number_of_steps; ++step) {  // MAD.hxx:158
+      if (d.verbose && d.number_of_steps > 1 && c_->comm.rank() == 0)
+        std::printf("\n------------ Time step n. %u / %u------------\n", step + 1, d.number_of_steps);
+      if (d.cycle == MAD_FMG) {
+        if (d.verbose && c_->comm.rank() == 0) std::printf("|--- Full Multigrid Cycle ---|\n");
+        to_fp32_rhs(b64_);
+        fmg_rec(0);  // MAD.hxx:170-176, in fp32
+        hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, c_->stream, L0.x, u64_, N);
+        HIP_CHECK(hipGetLastError());
+      } else {
+        HIP_CHECK(hipMemcpyAsync(u64_, b64_, sizeof(double) * N, hipMemcpyDeviceToDevice,
+                                 c_->stream));  // MAD.hxx:177-201
+      }
+      const double rhsNorm = norm64(b64_);  // MAD.hxx:204
+      REQUIRE(std::isfinite(rhsNorm), MAD_ERR_NUMERIC,
+              "non-finite right-hand side norm (NaN/Inf in the input image)");
+      double resNorm = residual64();
+      REQUIRE(std::isfinite(resNorm), MAD_ERR_NUMERIC,
+              "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
+      unsigned it = 0;
+      std::vector<double> hist;
+      const unsigned window = (d.cycle == MAD_SMOOTHER) ? 50 : 5;
+      bool stalled = false;
+      do {  // MAD.hxx:207-246
+        to_fp32_rhs(r64_);
+        fill(0, MAD_X, 0.0);
+        if (d.cycle == MAD_SMOOTHER) {
+          smooth(0, 1);
+        } else {
+          if (d.verbose && c_->comm.rank() == 0) std::printf("\n|--- VCycle n. %u ---|\n", it + 1);
+          vcycle_fast();
+        }
+        hipLaunchKernelGGL((add_conv_k<T>), dim3(nb), dim3(256), 0, c_->stream, u64_, L0.x, N);
+        HIP_CHECK(hipGetLastError());
+        resNorm = residual64();  // MAD.hxx:221-229
+        REQUIRE(std::isfinite(resNorm), MAD_ERR_NUMERIC,
+                "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
+        relres = (rhsNorm > 0.0) ? resNorm / rhsNorm : resNorm;
+        if (d.verbose && d.cycle == MAD_SMOOTHER && c_->comm.rank() == 0)
+          std::printf("Smoother iteration n. %u: relative residual = %g\n", it + 1, relres);
+        ++it;
+        hist.push_back(relres);
+        // fallback only: the fp64 residual keeps falling where plain fp32 stalls
+        if (d.stall_guard && hist.size() > window && relres < 1e-3) {
+          double prev_best = INFINITY;
+          for (size_t q = 0; q + window < hist.size(); ++q) prev_best = std::min(prev_best, hist[q]);
+          double recent = INFINITY;
+          for (size_t q = hist.size() - window; q < hist.size(); ++q) recent = std::min(recent, hist[q]);
+          if (recent > 0.99 * prev_best) stalled = true;
+        }
+      } while (relres > d.tolerance && it < d.max_cycles && !stalled);
+      stalled_any |= stalled;
+      total += it;
+      c_->step_cycles.push_back(it);
+      c_->step_relres.push_back(relres);
+      HIP_CHECK(hipMemcpyAsync(b64_, u64_, sizeof(double) * N, hipMemcpyDeviceToDevice,
+                               c_->stream));  // MAD.hxx:248-261
+    }
+    HIP_CHECK(hipEventRecord(e1, c_->stream));
+    void* dst = out;
+    if (!dev_io) dst = scratch_bytes(N * dtype_size(out_dtype));
+    convert_from(u64_, dst, out_dtype, N, c_->stream);  // MAD.hxx:266-289
     if (!dev_io)
       HIP_CHECK(hipMemcpyAsync(out, dst, N * dtype_size(out_dtype), hipMemcpyDeviceToHost,
                                c_->stream));
@@ -1633,6 +1828,17 @@ class Solver final : public SolverBase {
  private:
   mad_ctx* c_ = nullptr;
   std::vector<LevelData<T>> lv_;
+  // MAD_FP32_REFINE (T = float): level 0's iterate, rhs and residual in fp64 (same layout as
+  // the level arrays: margin + GHOST planes) and its operator as fp64 coefficient records
+  // with the reference's g (from the fp64 tensor); the fp32 hierarchy solves for corrections
+  bool refine_ = false;
+  double* r64alloc_[3] = {nullptr, nullptr, nullptr};
+  double* u64_ = nullptr;
+  double* b64_ = nullptr;
+  double* r64_ = nullptr;
+  double* cf64_alloc_ = nullptr;
+  double* cf64_ = nullptr;
+  Rat<double> rat64_{};
   int64_t part_cap_ = 0;             // entries of part_
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
   std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
@@ -1668,6 +1874,11 @@ class Solver final : public SolverBase {
       if (L.ct_alloc) (void)hipFree(L.ct_alloc);
     }
     lv_.clear();
+    for (auto& a : r64alloc_)
+      if (a) (void)hipFree(a), a = nullptr;
+    if (cf64_alloc_) (void)hipFree(cf64_alloc_);
+    cf64_alloc_ = nullptr;
+    u64_ = b64_ = r64_ = cf64_ = nullptr;
     if (part_) (void)hipFree(part_);
     if (scal_) (void)hipFree(scal_);
     if (hscal_) (void)hipHostFree(hscal_);
@@ -1795,6 +2006,44 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipStreamSynchronize(c_->stream));
         HIP_CHECK(hipFree(full_cf));
         full_cf = nullptr;
+      }
+      if (l == 0 && refine_) {
+        // the refined system's operator: fp64 records, g from the fp64 tensor (build_coef*_k
+        // restate GH.hxx:298-516 directly; no build_g_k pass), owned + ghost planes
+        double* full64 = cf64_;
+        if (slab) HIP_CHECK(hipMalloc(&full64, sizeof(double) * Ng * ncoef_));
+        if (dim == 3) {
+          const int bx = ((int)G.n[0] + 63) / 64, by = ((int)G.n[1] + 3) / 4;
+          const int nzg = (int)G.n[2];
+          int chunks = std::max(1, std::min(nzg, (4096 + bx * by - 1) / (bx * by)));
+          const int kc = (nzg + chunks - 1) / chunks;
+          chunks = (nzg + kc - 1) / kc;
+          auto go = [&](auto K) {
+            hipLaunchKernelGGL((build_coef3_k<double, decltype(K)::value>), dim3(bx, by, chunks), BLK, 0,
+                               c_->stream, fine, (int)G.n[0], (int)G.n[1], nzg,
+                               coef_factors(G.h, c_->d.time_step), full64, ncoef_, kc);
+          };
+          if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
+          else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
+          else go(std::integral_constant<int, KISO>{});
+        } else {
+          dispatch(dim, c_->kind, [&](auto D, auto K) {
+            hipLaunchKernelGGL((build_coef_k<double, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
+                               (int)G.n[0], (int)G.n[1], (int)G.n[2],
+                               coef_factors(G.h, c_->d.time_step), full64, ncoef_);
+          });
+        }
+        HIP_CHECK(hipGetLastError());
+        if (slab) {
+          const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
+          const int64_t p1 = std::min<int64_t>(G.z1 + GHOST, G.n[2]);
+          const int64_t cplane = L.g.sz * ncoef_;
+          HIP_CHECK(hipMemcpyAsync(cf64_ + (p0 - G.z0) * cplane, full64 + p0 * cplane,
+                                   sizeof(double) * (p1 - p0) * cplane, hipMemcpyDeviceToDevice,
+                                   c_->stream));
+          HIP_CHECK(hipStreamSynchronize(c_->stream));
+          HIP_CHECK(hipFree(full64));
+        }
       }
       if (L.ct) {
         // tensor records of every allocated plane the coefficient records hold
@@ -2130,7 +2379,8 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
     REQUIRE(d->cycle >= MAD_VCYCLE && d->cycle <= MAD_SMOOTHER, MAD_ERR_INVALID, "bad cycle");
     REQUIRE(d->smoother >= MAD_GAUSS_SEIDEL && d->smoother <= MAD_WEIGHTED_JACOBI,
             MAD_ERR_INVALID, "bad smoother");
-    REQUIRE(d->precision == MAD_FP32 || d->precision == MAD_FP64, MAD_ERR_INVALID,
+    REQUIRE(d->precision == MAD_FP32 || d->precision == MAD_FP64 || d->precision == MAD_FP32_REFINE,
+            MAD_ERR_INVALID,
             "bad precision");
     REQUIRE(d->nranks >= 1 && d->rank >= 0 && d->rank < d->nranks, MAD_ERR_INVALID,
             "bad rank / nranks");

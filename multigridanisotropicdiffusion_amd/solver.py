@@ -84,7 +84,7 @@ class Solver:
         d.omega = float(omega)
         d.verbose = int(bool(verbose))
         d.precision = int(precision)
-        d.stall_guard = int(precision == C.FP32) if stall_guard is None else int(stall_guard)
+        d.stall_guard = int(precision != C.FP64) if stall_guard is None else int(stall_guard)
         d.device = int(device)
         d.tensor_kind = int(tensor_kind)
         d.nranks = int(nranks)

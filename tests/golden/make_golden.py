@@ -8,6 +8,12 @@ Inputs
                     test/itk2DDiffusionTest_GS.cxx:21-42)
   ved_crop_i16.npy  35x39x35 crop (z,y,x) of test/test_data/ved_test.zraw (zlib,
                     int16, DimSize 69 77 69, spacing .3125 .3125 .5)
+  ved2_crop_i16.npy 55x52x54 centre crop (z,y,x) of test/test_data/ved_test_2.zraw (zlib,
+                    int16, DimSize 134 140 119, spacing .330017): its hierarchy coarsens
+                    CCV -> VCC -> CVC (x,y,z), the first three of the full volume's
+                    CCV -> VCC -> CVC -> VCV
+  (python tests/golden/make_golden.py ved2   regenerates only the ved_test_2 fixtures,
+   python tests/golden/make_golden.py lena64 only the fp64 lena solutions lena_c1_f64.npz)
 Expected outputs come from the fp64 oracle (oracle/), which restates the
 reference line by line.  PARITY UNPINNED: the reference has no golden vectors
 of its own and cannot be built here, so these pin the GPU path to the oracle
@@ -38,6 +44,29 @@ def make_inputs():
     raw = zlib.decompress(open(os.path.join(REF, "ved_test.zraw"), "rb").read())
     ved = np.frombuffer(raw, dtype="<i2").reshape(69, 77, 69)  # (z, y, x)
     np.save(os.path.join(HERE, "ved_crop_i16.npy"), np.ascontiguousarray(ved[17:52, 19:58, 17:52]))
+    make_ved2_input()
+
+
+VED2_SPACING = (0.330017, 0.330017, 0.330017)
+
+
+def make_ved2_input():
+    raw = zlib.decompress(open(os.path.join(REF, "ved_test_2.zraw"), "rb").read())
+    v2 = np.frombuffer(raw, dtype="<i2").reshape(119, 140, 134)  # (z, y, x)
+    np.save(os.path.join(HERE, "ved2_crop_i16.npy"), np.ascontiguousarray(v2[32:87, 44:96, 40:94]))
+
+
+def ved2_mad():
+    """itkVEDTest_GS MAD parameters (nu 3, dt 0.1, 4 steps, tolerance 1e-10, lexicographic GS;
+    test/itkVEDTest_GS.cxx:61,84-88) on the ved_test_2 crop with a VED-form tensor."""
+    v2 = np.load(os.path.join(HERE, "ved2_crop_i16.npy")).astype(np.float64)
+    T = synth.ved_form(v2.shape)
+    o = O.Oracle(v2.shape, VED2_SPACING, T, 0.1)
+    out, c, rr = o.run(v2, cycle=O.VCYCLE, smoother=O.GS_LEX, tolerance=1e-10,
+                       iterations_per_grid=3, number_of_steps=4)
+    print("ved2", [lv["shape"] for lv in o.levels], c, rr)
+    np.savez_compressed(os.path.join(HERE, "ved2_mad.npz"), out=out, cycles=np.array(c),
+                        relres=np.array(rr), spacing=np.array(VED2_SPACING))
 
 
 # per-kernel cases: (name, shape, spacing x-first, tensor maker, dt)
@@ -85,7 +114,31 @@ def kernel_case(name, shape, spacing, tmaker, dt):
     return d
 
 
+def lena_f64():
+    """C1 (itk2DDiffusionTest_{GS,WJ}) oracle solutions in fp64 (lena_c1.npz keeps them in
+    fp32): the references of the MAD_FP32_REFINE tests, which resolve 1e-9."""
+    lena = np.load(os.path.join(HERE, "lena_256_u8.npy")).astype(np.float64)
+    T = synth.constant(lena.shape, (50.0, 0.0, 30.0))
+    o = O.Oracle(lena.shape, (1.0, 1.0), T, 0.1)
+    res = {}
+    for sm, tag in ((O.WJ, "wj"), (O.GS_LEX, "gs")):
+        for cyc, ctag in ((O.VCYCLE, "v"), (O.FMG, "fmg")):
+            out, c, rr = o.run(lena, cycle=cyc, smoother=sm, tolerance=1e-10, iterations_per_grid=2)
+            res[f"{tag}_{ctag}"] = out
+            res[f"{tag}_{ctag}_cycles"] = np.array(c)
+            res[f"{tag}_{ctag}_relres"] = np.array(rr)
+    np.savez_compressed(os.path.join(HERE, "lena_c1_f64.npz"), **res)
+
+
 def main():
+    if sys.argv[1:] == ["lena64"]:
+        lena_f64()
+        return
+    if sys.argv[1:] == ["ved2"]:
+        if os.path.isdir(REF):
+            make_ved2_input()
+        ved2_mad()
+        return
     if os.path.isdir(REF):
         make_inputs()
     for case in KERNEL_CASES:
@@ -104,6 +157,7 @@ def main():
             res[f"{tag}_{ctag}_cycles"] = np.array(c)
             print("lena", tag, ctag, c, rr)
     np.savez_compressed(os.path.join(HERE, "lena_c1.npz"), **res)
+    lena_f64()
     # VED-test MAD parameters on the ved crop with a VED-form tensor:
     # nu 3, dt 0.1, 4 steps (test/itkVEDTest_GS.cxx:61,84-88), spacing .3125 .3125 .5
     ved = np.load(os.path.join(HERE, "ved_crop_i16.npy")).astype(np.float64)
@@ -115,6 +169,7 @@ def main():
     print("ved", c, rr)
     np.savez_compressed(os.path.join(HERE, "ved_mad.npz"), out=out, cycles=np.array(c),
                         spacing=np.array(sp))
+    ved2_mad()
 
 
 if __name__ == "__main__":

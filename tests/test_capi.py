@@ -82,7 +82,7 @@ def _plan(shape, spacing=None, nranks=1, rank=0):
             return out
 
 
-@pytest.mark.parametrize("shape", [(69, 77, 69), (119, 140, 134), (24, 26, 28), (256, 256)])
+@pytest.mark.parametrize("shape", [(69, 77, 69), (119, 140, 134), (55, 52, 54), (24, 26, 28), (256, 256)])
 def test_plan_matches_oracle_hierarchy(oracle_mod, shape):
     T = np.stack([np.ones(shape)] * (3 if len(shape) == 2 else 6))
     o = oracle_mod.Oracle(shape, [1.0] * len(shape), T, 0.1)

@@ -1,0 +1,111 @@
+"""MAD_FP32_REFINE: fp32 hierarchy (all smoothing, transfer and coarse kernels in fp32) inside a
+mixed-precision defect correction -- level 0's iterate, rhs and residual in fp64 with the fp64
+operator, one fp32 cycle on the error equation per correction.  The bar (VERDICT round 1,
+item 5): the reference's own tolerance 1e-10 (test/itk2DDiffusionTest_GS.cxx:97,
+test/itkVEDTest_GS.cxx:85) is reached -- plain fp32 stalls near 1e-7 -- and the solution
+matches the oracle as closely as an fp64 solve does.  Cycle counts sit beside the oracle's
+(lexicographic GS) and the GPU's fp64 solve (multicolour GS)."""
+import os
+
+import numpy as np
+import pytest
+
+import synth
+from conftest import GOLDEN, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def relinf(a, ref):
+    return np.abs(np.asarray(a, np.float64) - ref).max() / np.abs(ref).max()
+
+
+@pytest.fixture(scope="module")
+def M():
+    import multigridanisotropicdiffusion_amd as mod
+    return mod
+
+
+def lena_run(M, precision, smoother, cycle):
+    lena = np.load(os.path.join(GOLDEN, "lena_256_u8.npy")).astype(np.float64)
+    T = np.stack([np.full(lena.shape, 50.0), np.zeros(lena.shape), np.full(lena.shape, 30.0)], axis=-1)
+    s = M.Solver(lena.shape, (1.0, 1.0), time_step=0.1, smoother=smoother, cycle=cycle,
+                 iterations_per_grid=2, max_cycles=100, tolerance=1e-10, precision=precision)
+    s.set_tensor(T)
+    out, st = s.run(lena, out_dtype=np.float64)
+    s.close()
+    return out, st
+
+
+@pytest.mark.parametrize("smoother,cycle,key", [("WJ", "VCYCLE", "wj_v"), ("WJ", "FMG", "wj_fmg"),
+                                                ("GS", "VCYCLE", "gs_v"), ("GS", "FMG", "gs_fmg")])
+def test_lena_c1_reaches_reference_tolerance(M, smoother, cycle, key):
+    """itk2DDiffusionTest_{GS,WJ}_{V,FMG} (C1: lena 256^2, M = diag(50, 30), dt 0.1, nu 2,
+    Tolerance 1e-10): fp32 kernels + fp64 correction reach relres <= 1e-10 without the stall
+    guard, and the solution equals the fp64 GPU solve to 1e-9 and the oracle to 1e-8."""
+    golden = load_golden("lena_c1_f64")
+    sm = M.WEIGHTED_JACOBI if smoother == "WJ" else M.GAUSS_SEIDEL
+    cy = getattr(M, cycle)
+    out, st = lena_run(M, M.FP32_REFINE, sm, cy)
+    out64, st64 = lena_run(M, M.FP64, sm, cy)
+    cyc = (st["total_cycles"], st64["total_cycles"], int(golden[key + "_cycles"][0]))
+    assert st["last_relres"] <= 1e-10 and not st["stalled"], (st["last_relres"], cyc)
+    assert relinf(out, out64) < 1e-9, cyc
+    assert relinf(out, golden[key]) < 1e-8, cyc
+    # one cycle more than the fp64 solve at most (the fp32 correction's rounding)
+    assert st["total_cycles"] <= st64["total_cycles"] + 1, cyc
+
+
+@pytest.mark.parametrize("fixture,crop,spacing", [
+    ("ved_mad", "ved_crop_i16.npy", (0.3125, 0.3125, 0.5)),
+    ("ved2_mad", "ved2_crop_i16.npy", (0.330017, 0.330017, 0.330017)),
+])
+def test_ved_parameters_reach_reference_tolerance(M, fixture, crop, spacing):
+    """itkVEDTest_GS MAD parameters (nu 3, dt 0.1, 4 steps, Tolerance 1e-10) on the ved_test
+    and ved_test_2 crops: every step converges to 1e-10 with fp32 kernels, and the result
+    equals the oracle's fp64 lexicographic solve to 1e-8 (the fp64 GPU solve's own bar)."""
+    v = np.load(os.path.join(GOLDEN, crop))
+    golden = load_golden(fixture)
+    s = M.Solver(v.shape, spacing, time_step=0.1, iterations_per_grid=3, number_of_steps=4,
+                 tolerance=1e-10, precision=M.FP32_REFINE)
+    s.set_tensor(synth.ved_form(v.shape))
+    out, st = s.run(v, out_dtype=np.float64)
+    s.close()
+    cyc = (list(st["step_cycles"]), [int(c) for c in golden["cycles"]])
+    assert st["steps"] == 4 and not st["stalled"], cyc
+    assert st["last_relres"] <= 1e-10, (st["last_relres"], cyc)
+    assert relinf(out, golden["out"]) < 1e-8, cyc
+    assert all(abs(int(a) - int(b)) <= 1 for a, b in zip(st["step_cycles"], golden["cycles"])), cyc
+
+
+def test_plain_fp32_stalls_where_refine_converges(M):
+    """The contrast: plain fp32 ends at its rounding floor (stall guard) above 1e-10 on the
+    same C1 solve that the refined mode converges."""
+    out, st = lena_run(M, M.FP32, M.GAUSS_SEIDEL, M.VCYCLE)
+    assert st["last_relres"] > 1e-10 and st["stalled"]
+
+
+def test_refine_rank_slabs_match_single(M):
+    """Refined runs on z-slabs (in-process transport, 2 ranks): the fp64 residual's halo and
+    norm allreduce; same cycle counts and result within 1e-12 of the single-rank run."""
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (64, 48, 40)
+    T = synth.ved_form(shape)
+    img = synth.image(shape, seed=5) * 100
+    sl = D.slabs(shape, 2)
+    kw = dict(time_step=0.4, tolerance=1e-10, precision=M.FP32_REFINE, number_of_steps=2)
+    s = M.Solver(shape, **kw)
+    s.set_tensor(T)
+    ref, rst = s.run(img, out_dtype=np.float64)
+    s.close()
+
+    def body(r, s):
+        s.set_tensor(T)
+        s.setup()
+        z0, z1 = sl[r]
+        return s.run(img[z0:z1], out_dtype=np.float64)
+    outs = D.run_local(2, body, shape, **kw)
+    full = np.concatenate([o[0] for o in outs])
+    assert rst["last_relres"] <= 1e-10
+    assert np.abs(full - ref).max() <= 1e-12 * np.abs(ref).max()
+    assert all(list(o[1]["step_cycles"]) == list(rst["step_cycles"]) for o in outs)
