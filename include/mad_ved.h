@@ -58,8 +58,17 @@ typedef struct mad_ved_desc {
   int32_t device;                  /* HIP device, -1 = current */
   int32_t nranks;                  /* z-slab ranks of the diffusion step (1 = single GPU) */
   int32_t rank;
-  int32_t reserved[6];
+  int32_t hessian;                 /* mad_ved_hessian_kind: MAD_VED_HESSIAN_RECURSIVE (default, the
+                                      reference's HessianRecursiveGaussianImageFilter operator,
+                                      VED.hxx:158-173) or MAD_VED_HESSIAN_FIR (sampled Gaussian
+                                      derivative taps, round 1) */
+  int32_t reserved[5];
 } mad_ved_desc;
+
+typedef enum mad_ved_hessian_kind {
+  MAD_VED_HESSIAN_RECURSIVE = 0,
+  MAD_VED_HESSIAN_FIR = 1
+} mad_ved_hessian_kind;
 
 typedef struct mad_ved_stats {
   uint32_t iterations;             /* VED iterations run */

@@ -23,6 +23,8 @@ GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, WEIGHTED_JACOBI = 0, 1, 2
 U8, I8, U16, I16, U32, I32, F32, F64 = range(8)
 # mad_precision
 FP32, FP64, FP32_REFINE = 0, 1, 2
+# mad_ved_hessian_kind
+VED_HESSIAN_RECURSIVE, VED_HESSIAN_FIR = 0, 1
 # mad_tensor_kind
 TENSOR_AUTO, TENSOR_ISOTROPIC, TENSOR_DIAGONAL, TENSOR_FULL = range(4)
 # mad_which
@@ -119,7 +121,8 @@ class VedDesc(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("nranks", ctypes.c_int32),
         ("rank", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("hessian", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 

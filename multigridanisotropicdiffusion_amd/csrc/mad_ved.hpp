@@ -16,6 +16,7 @@ struct mad_ved_ctx {
   double* img = nullptr;   // internal image (fp64, VED.h:61)
   double* img2 = nullptr;  // next iterate
   void* fir = nullptr;     // 9 FIR volumes in the storage precision
+  double* iir = nullptr;   // 12 fp64 volumes of the recursive Hessian passes
   void* taps = nullptr;    // per-axis taps of the current scale (device)
   double* resp = nullptr;  // m_MaxVesselnessResponse
   double* dir = nullptr;   // vessel direction (eigenvector column 2 of the max scale), SoA x3
@@ -24,7 +25,7 @@ struct mad_ved_ctx {
   ~mad_ved_ctx() {
     if (mad) (void)hipSetDevice(mad->device);
     if (mad && mad->stream) (void)hipStreamSynchronize(mad->stream);
-    for (void* p : {(void*)img, (void*)img2, fir, taps, (void*)resp, (void*)dir, stage})
+    for (void* p : {(void*)img, (void*)img2, fir, (void*)iir, taps, (void*)resp, (void*)dir, stage})
       if (p) (void)hipFree(p);
     if (mad) mad_destroy(mad);
   }
@@ -122,9 +123,177 @@ void ved_lds_attr() {
   done = true;
 }
 
+// ITK RecursiveGaussianImageFilter coefficients of one axis / order, sigma sd in voxels
+// (restates oracle/ved_oracle.py recursive_coefficients, same formulas and order)
+IirCoef ved_iir_coef(double sd, int order) {
+  const double A1[3] = {1.3530, -0.6724, -1.3563}, B1[3] = {1.8151, -3.4327, 5.2318};
+  const double W1 = 0.6681, L1 = -1.3932;
+  const double A2[3] = {-0.3531, 0.6724, 0.3446}, B2[3] = {0.0902, 0.6100, -2.2355};
+  const double W2 = 2.0787, L2 = -1.3732;
+  auto ncoef = [&](int o, double N[4], double& SN, double& DN, double& EN) {
+    const double a1 = A1[o], b1 = B1[o], a2 = A2[o], b2 = B2[o];
+    const double s1 = std::sin(W1 / sd), s2 = std::sin(W2 / sd);
+    const double c1 = std::cos(W1 / sd), c2 = std::cos(W2 / sd);
+    const double e1 = std::exp(L1 / sd), e2 = std::exp(L2 / sd);
+    N[0] = a1 + a2;
+    N[1] = e2 * (b2 * s2 - (a2 + 2 * a1) * c2);
+    N[1] += e1 * (b1 * s1 - (a1 + 2 * a2) * c1);
+    N[2] = (a1 + a2) * c2 * c1;
+    N[2] -= b1 * c2 * s1 + b2 * c1 * s2;
+    N[2] *= 2 * e1 * e2;
+    N[2] += a2 * e1 * e1 + a1 * e2 * e2;
+    N[3] = e2 * e1 * e1 * (b2 * s2 - a2 * c2);
+    N[3] += e1 * e2 * e2 * (b1 * s1 - a1 * c1);
+    SN = N[0] + N[1] + N[2] + N[3];
+    DN = N[1] + 2 * N[2] + 3 * N[3];
+    EN = N[1] + 4 * N[2] + 9 * N[3];
+  };
+  IirCoef C{};
+  double* D = C.d;
+  {
+    const double c1 = std::cos(W1 / sd), c2 = std::cos(W2 / sd);
+    const double e1 = std::exp(L1 / sd), e2 = std::exp(L2 / sd);
+    D[3] = e1 * e1 * e2 * e2;
+    D[2] = -2 * c1 * e1 * e2 * e2;
+    D[2] += -2 * c2 * e2 * e1 * e1;
+    D[1] = 4 * c2 * c1 * e1 * e2;
+    D[1] += e1 * e1 + e2 * e2;
+    D[0] = -2 * (e2 * c2 + e1 * c1);
+  }
+  const double SD = 1.0 + D[0] + D[1] + D[2] + D[3];
+  const double DD = D[0] + 2 * D[1] + 3 * D[2] + 4 * D[3];
+  const double ED = D[0] + 4 * D[1] + 9 * D[2] + 16 * D[3];
+  double* N = C.n;
+  bool symmetric = true;
+  if (order == 0) {
+    double SN, DN, EN;
+    ncoef(0, N, SN, DN, EN);
+    const double alpha = 2 * SN / SD - N[0];
+    for (int q = 0; q < 4; ++q) N[q] = N[q] / alpha;
+  } else if (order == 1) {
+    double SN, DN, EN;
+    ncoef(1, N, SN, DN, EN);
+    const double alpha = 2 * (SN * DD - DN * SD) / (SD * SD);
+    for (int q = 0; q < 4; ++q) N[q] = N[q] / alpha;
+    symmetric = false;
+  } else {
+    double N0[4], N2[4], SN0, DN0, EN0, SN2, DN2, EN2;
+    ncoef(0, N0, SN0, DN0, EN0);
+    ncoef(2, N2, SN2, DN2, EN2);
+    const double beta = -(2 * SN2 - SD * N2[0]) / (2 * SN0 - SD * N0[0]);
+    double abcd[4];
+    for (int q = 0; q < 4; ++q) abcd[q] = N2[q] + beta * N0[q];
+    const double SN = abcd[0] + abcd[1] + abcd[2] + abcd[3];
+    const double DN = abcd[1] + 2 * abcd[2] + 3 * abcd[3];
+    const double EN = abcd[1] + 4 * abcd[2] + 9 * abcd[3];
+    double alpha = EN * SD * SD - ED * SN * SD - 2 * DN * DD * SD + 2 * DD * DD * SN;
+    alpha /= SD * SD * SD;
+    for (int q = 0; q < 4; ++q) N[q] = abcd[q] / alpha;
+  }
+  double* M = C.m;
+  if (symmetric) {
+    M[0] = N[1] - D[0] * N[0];
+    M[1] = N[2] - D[1] * N[0];
+    M[2] = N[3] - D[2] * N[0];
+    M[3] = -D[3] * N[0];
+  } else {
+    M[0] = -(N[1] - D[0] * N[0]);
+    M[1] = -(N[2] - D[1] * N[0]);
+    M[2] = -(N[3] - D[2] * N[0]);
+    M[3] = D[3] * N[0];
+  }
+  const double SNn = N[0] + N[1] + N[2] + N[3];
+  const double SM = M[0] + M[1] + M[2] + M[3];
+  const double SDn = 1.0 + D[0] + D[1] + D[2] + D[3];
+  for (int q = 0; q < 4; ++q) {
+    C.bn[q] = D[q] * SNn / SDn;
+    C.bm[q] = D[q] * SM / SDn;
+  }
+  return C;
+}
+
+// one scale with the recursive (IIR) operator: z pass (image -> orders 0..2), y pass (-> the
+// six (y, z) order pairs), x pass (-> the six scaled Hessian components), then the Hessian
+// out (VED_HESSIAN) or UpdateVesselness (VED_UPDATE) per voxel
+template <typename T>
+void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess) {
+  hipStream_t st = v->mad->stream;
+  const int nx = (int)v->n[0], ny = (int)v->n[1], nz = (int)v->n[2];
+  REQUIRE(nx >= 4 && ny >= 4 && nz >= 4, MAD_ERR_UNSUPPORTED,
+          "the recursive Gaussian needs at least 4 points along each axis");
+  const int64_t N = v->N;
+  if (!v->iir) HIP_CHECK(hipMalloc(&v->iir, sizeof(double) * 12 * N));
+  // slots: Z 0..2, pairs A 6..11, Hessian 0..5 (over the dead Z: one SoA block)
+  double* Z[3] = {v->iir, v->iir + N, v->iir + 2 * N};
+  double* A[6];
+  double* H[6];
+  for (int q = 0; q < 6; ++q) {
+    A[q] = v->iir + (6 + q) * N;
+    H[q] = v->iir + q * N;
+  }
+  const double* h = v->d.spacing;
+  auto launch = [&](const IirPass& P, int axis) {
+    const int64_t lines = axis == 0 ? (int64_t)ny * nz : axis == 1 ? (int64_t)nx * nz : (int64_t)nx * ny;
+    hipLaunchKernelGGL(ved_iir_k, dim3((unsigned)((lines + 255) / 256)), dim3(256), 0, st, P, axis, nx, ny, nz);
+    HIP_CHECK(hipGetLastError());
+  };
+  IirPass P{};
+  // z: image -> Z_o, o = 0, 1, 2
+  P.in[0] = v->img;
+  P.nout = 3;
+  for (int o = 0; o < 3; ++o) {
+    P.out[o] = Z[o];
+    P.src[o] = 0;
+    P.c[o] = ved_iir_coef(sigma / h[2], o);
+    P.scale[o] = 1.0;
+  }
+  launch(P, 2);
+  // y: (oy, oz) = (0,0) (1,0) (2,0) (0,1) (1,1) (0,2)
+  const int pairs[6][2] = {{0, 0}, {1, 0}, {2, 0}, {0, 1}, {1, 1}, {0, 2}};
+  P = IirPass{};
+  for (int q = 0; q < 3; ++q) P.in[q] = Z[q];
+  P.nout = 6;
+  for (int q = 0; q < 6; ++q) {
+    P.out[q] = A[q];
+    P.src[q] = pairs[q][1];
+    P.c[q] = ved_iir_coef(sigma / h[1], pairs[q][0]);
+    P.scale[q] = 1.0;
+  }
+  launch(P, 1);
+  // x: H = [xx, xy, xz, yy, yz, zz] from (ox, pair) and sigma^2 / (h_i h_j)
+  const int xsrc[6] = {0, 1, 3, 2, 4, 5};  // pair index feeding each component
+  const int xord[6] = {2, 1, 1, 0, 0, 0};
+  const int cd[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+  P = IirPass{};
+  for (int q = 0; q < 6; ++q) P.in[q] = A[q];
+  P.nout = 6;
+  const double s2 = sigma * sigma;
+  for (int q = 0; q < 6; ++q) {
+    P.out[q] = H[q];
+    P.src[q] = xsrc[q];
+    P.c[q] = ved_iir_coef(sigma / h[0], xord[q]);
+    P.scale[q] = s2 / (h[cd[q][0]] * h[cd[q][1]]);
+  }
+  launch(P, 0);
+  const double* Hs = H[0];
+  const VesselParams vp{v->d.alpha, v->d.beta, v->d.gamma};
+  const unsigned nb = flat_blocks(N);
+  if (mode == VED_HESSIAN)
+    hipLaunchKernelGGL((ved_hess_k<T, VED_HESSIAN>), dim3(nb), dim3(256), 0, st, Hs, N, hess, nullptr,
+                       nullptr, 0, vp);
+  else
+    hipLaunchKernelGGL((ved_hess_k<T, VED_UPDATE>), dim3(nb), dim3(256), 0, st, Hs, N, nullptr, v->resp,
+                       v->dir, first ? 1 : 0, vp);
+  HIP_CHECK(hipGetLastError());
+}
+
 // one scale: Hessian (MODE VED_HESSIAN, into `hess`) or vesselness update
 template <typename T>
 void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess) {
+  if (v->d.hessian == MAD_VED_HESSIAN_RECURSIVE) {
+    ved_scale_iir<T>(v, sigma, mode, first, hess);
+    return;
+  }
   hipStream_t st = v->mad->stream;
   const int nx = (int)v->n[0], ny = (int)v->n[1], nz = (int)v->n[2];
   const int64_t N = v->N;
@@ -312,6 +481,8 @@ int mad_ved_create(const mad_ved_desc* d, mad_ved_ctx** out) {
   int rc = ved_guarded(nullptr, [&] {
     REQUIRE(d, MAD_ERR_INVALID, "null descriptor");
     REQUIRE(d->abi_version == MAD_ABI_VERSION, MAD_ERR_INVALID, "ABI version mismatch");
+    REQUIRE(d->hessian == MAD_VED_HESSIAN_RECURSIVE || d->hessian == MAD_VED_HESSIAN_FIR,
+            MAD_ERR_INVALID, "bad Hessian kind");
     REQUIRE(d->nscales >= 1 && d->nscales <= MAD_VED_MAX_SCALES, MAD_ERR_INVALID,
             "nscales must be 1.." + std::to_string(MAD_VED_MAX_SCALES));
     for (int s = 0; s < d->nscales; ++s)

@@ -1,7 +1,8 @@
 // mad_ved_kernels.hpp -- device kernels of the VED tensor generation (include/mad_ved.h).
 //
 // Reference: include/itkVEDMultigridImageFilter.hxx (VED.hxx below).
-//   ComputeHessian          VED.hxx:158-173  -> ved_fir_{z,y}_k + ved_fir_x_k
+//   ComputeHessian          VED.hxx:158-173  -> ved_iir_k (x3 axes; ITK's recursive operator,
+//                                              default) or ved_fir_{z,y}_k + ved_fir_x_k
 //   VesselnessFunction      VED.hxx:176-212  -> ved_vesselness
 //   UpdateVesselness        VED.hxx:215-299  -> ved_fir_x_k<.., VED_UPDATE> (fused)
 //   GenerateDiffusionTensor VED.hxx:302-378  -> ved_tensor_k
@@ -315,6 +316,12 @@ __device__ inline E ved_vesselness(E e0, E e1, E e2, const VesselParams& vp) {
 
 enum { VED_HESSIAN = 0, VED_UPDATE = 1 };
 
+template <typename T, int MODE>
+__device__ __forceinline__ void ved_point(double H0, double H1, double H2, double H3, double H4,
+                                          double H5, int64_t p, int64_t n, double* __restrict__ hess,
+                                          double* __restrict__ resp, double* __restrict__ dir,
+                                          int first, const VesselParams& vp);
+
 // x pass + (MODE == VED_HESSIAN) write the scale-normalised Hessian, fp64 SoA, or
 // (MODE == VED_UPDATE) UpdateVesselness: eigen-analysis, vesselness, keep the response
 // and the eigenvector of the largest (algebraic) eigenvalue -- the column
@@ -366,7 +373,17 @@ __global__ void __launch_bounds__(256) ved_fir_x_k(const T* __restrict__ a00, co
   }
   const double H0 = (double)hxx * hs.f[0], H1 = (double)hxy * hs.f[1], H2 = (double)hxz * hs.f[2];
   const double H3 = (double)hyy * hs.f[3], H4 = (double)hyz * hs.f[4], H5 = (double)hzz * hs.f[5];
-  const int64_t p = row + i;
+  ved_point<T, MODE>(H0, H1, H2, H3, H4, H5, row + i, n, hess, resp, dir, first, vp);
+}
+
+// one voxel's scale-normalised Hessian [xx,xy,xz,yy,yz,zz] (fp64): written out (MODE
+// VED_HESSIAN) or UpdateVesselness (VED_UPDATE), see ved_fir_x_k
+template <typename T, int MODE>
+__device__ __forceinline__ void ved_point(double H0, double H1, double H2, double H3, double H4,
+                                          double H5, int64_t p, int64_t n, double* __restrict__ hess,
+                                          double* __restrict__ resp, double* __restrict__ dir,
+                                          int first, const VesselParams& vp) {
+#pragma clang fp contract(off)
   if (MODE == VED_HESSIAN) {
     hess[p] = H0;
     hess[n + p] = H1;
@@ -414,6 +431,125 @@ __global__ void __launch_bounds__(256) ved_fir_x_k(const T* __restrict__ a00, co
     dir[n + p] = (double)d[1];
     dir[2 * n + p] = (double)d[2];
   }
+}
+
+// ---------------------------------------------------------------------------
+// ITK's HessianRecursiveGaussianImageFilter operator (the reference's ComputeHessian,
+// VED.hxx:158-173): per axis a recursive (IIR) Gaussian / derivative filter, ITK
+// RecursiveGaussianImageFilter's algorithm (Deriche 4th order; coefficients computed on the
+// host, ved_iir_coef in mad_ved.hpp, restating oracle/ved_oracle.py recursive_coefficients).
+// One thread per line: a causal pass (initial state: the first value extends to -infinity)
+// writes the output, an anticausal pass (last value to +infinity) adds its part, then the
+// output is scaled (x pass: sigma^2 / (h_i h_j)).  fp64 throughout (ITK's RealType), the
+// arithmetic in the oracle's order with contraction off.
+struct IirCoef {
+  double n[4], m[4], d[4], bn[4], bm[4];
+};
+struct IirPass {
+  const double* in[6];
+  double* out[6];
+  int src[6];       // input of each output
+  IirCoef c[6];     // its filter along this pass's axis
+  double scale[6];  // applied to the finished output
+  int nout;
+};
+
+__global__ void __launch_bounds__(256) ved_iir_k(IirPass P, int axis, int nx, int ny, int nz) {
+#pragma clang fp contract(off)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t base, st;
+  int n;
+  if (axis == 0) {  // lines along x, one per (y, z)
+    if (t >= (int64_t)ny * nz) return;
+    base = t * nx;
+    st = 1;
+    n = nx;
+  } else if (axis == 1) {  // along y, one per (x, z): consecutive threads, consecutive x
+    if (t >= (int64_t)nx * nz) return;
+    const int64_t i = t % nx, k = t / nx;
+    base = k * nx * ny + i;
+    st = nx;
+    n = ny;
+  } else {  // along z, one per (x, y)
+    if (t >= (int64_t)nx * ny) return;
+    base = t;
+    st = (int64_t)nx * ny;
+    n = nz;
+  }
+  for (int o = 0; o < P.nout; ++o) {
+    const double* x = P.in[P.src[o]] + base;
+    double* y = P.out[o] + base;
+    const IirCoef& c = P.c[o];
+    const double N0 = c.n[0], N1 = c.n[1], N2 = c.n[2], N3 = c.n[3];
+    const double D1 = c.d[0], D2 = c.d[1], D3 = c.d[2], D4 = c.d[3];
+    // causal
+    {
+      const double v = x[0], x1 = x[st], x2 = x[2 * st], x3 = x[3 * st];
+      double s0 = v * N0 + v * N1 + v * N2 + v * N3;
+      double s1 = x1 * N0 + v * N1 + v * N2 + v * N3;
+      double s2 = x2 * N0 + x1 * N1 + v * N2 + v * N3;
+      double s3 = x3 * N0 + x2 * N1 + x1 * N2 + v * N3;
+      s0 -= v * c.bn[0] + v * c.bn[1] + v * c.bn[2] + v * c.bn[3];
+      s1 -= s0 * D1 + v * c.bn[1] + v * c.bn[2] + v * c.bn[3];
+      s2 -= s1 * D1 + s0 * D2 + v * c.bn[2] + v * c.bn[3];
+      s3 -= s2 * D1 + s1 * D2 + s0 * D3 + v * c.bn[3];
+      y[0] = s0;
+      y[st] = s1;
+      y[2 * st] = s2;
+      y[3 * st] = s3;
+      double xm1 = x3, xm2 = x2, xm3 = x1, sm1 = s3, sm2 = s2, sm3 = s1, sm4 = s0;
+      for (int i = 4; i < n; ++i) {
+        const double xi = x[i * st];
+        double si = xi * N0 + xm1 * N1 + xm2 * N2 + xm3 * N3;
+        si -= sm1 * D1 + sm2 * D2 + sm3 * D3 + sm4 * D4;
+        y[i * st] = si;
+        xm3 = xm2; xm2 = xm1; xm1 = xi;
+        sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = si;
+      }
+    }
+    // anticausal, added to the causal part, then scaled
+    {
+      const double M1 = c.m[0], M2 = c.m[1], M3 = c.m[2], M4 = c.m[3];
+      const double sc = P.scale[o];
+      const double v = x[(int64_t)(n - 1) * st];
+      const double xa = v, xb = x[(int64_t)(n - 2) * st], xc = x[(int64_t)(n - 3) * st];
+      double a1 = v * M1 + v * M2 + v * M3 + v * M4;                  // a[n-1]
+      double a2 = xa * M1 + v * M2 + v * M3 + v * M4;                 // a[n-2]
+      double a3 = xb * M1 + xa * M2 + v * M3 + v * M4;                // a[n-3]
+      double a4 = xc * M1 + xb * M2 + xa * M3 + v * M4;               // a[n-4]
+      a1 -= v * c.bm[0] + v * c.bm[1] + v * c.bm[2] + v * c.bm[3];
+      a2 -= a1 * D1 + v * c.bm[1] + v * c.bm[2] + v * c.bm[3];
+      a3 -= a2 * D1 + a1 * D2 + v * c.bm[2] + v * c.bm[3];
+      a4 -= a3 * D1 + a2 * D2 + a1 * D3 + v * c.bm[3];
+      double* yp = y + (int64_t)(n - 1) * st;
+      yp[0] = (yp[0] + a1) * sc;
+      yp[-st] = (yp[-st] + a2) * sc;
+      yp[-2 * st] = (yp[-2 * st] + a3) * sc;
+      yp[-3 * st] = (yp[-3 * st] + a4) * sc;
+      // window: x[i], x[i+1], x[i+2], x[i+3] and a[i], a[i+1], a[i+2], a[i+3], from i = n-4
+      double w0 = x[(int64_t)(n - 4) * st], w1 = xc, w2 = xb, w3 = xa;
+      double b0 = a4, b1 = a3, b2 = a2, b3 = a1;
+      for (int i = n - 4; i > 0; --i) {
+        double ai = w0 * M1 + w1 * M2 + w2 * M3 + w3 * M4;  // a[i-1]
+        ai -= b0 * D1 + b1 * D2 + b2 * D3 + b3 * D4;
+        double* yi = y + (int64_t)(i - 1) * st;
+        yi[0] = (yi[0] + ai) * sc;
+        w3 = w2; w2 = w1; w1 = w0; w0 = x[(int64_t)(i - 1) * st];
+        b3 = b2; b2 = b1; b1 = b0; b0 = ai;
+      }
+    }
+  }
+}
+
+// UpdateVesselness / Hessian output from the six recursive-Hessian volumes
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) ved_hess_k(const double* __restrict__ H, int64_t n,
+                                                  double* __restrict__ hess, double* __restrict__ resp,
+                                                  double* __restrict__ dir, int first, VesselParams vp) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x)
+    ved_point<T, MODE>(H[p], H[n + p], H[2 * n + p], H[3 * n + p], H[4 * n + p], H[5 * n + p], p, n,
+                       hess, resp, dir, first, vp);
 }
 
 // GenerateDiffusionTensor (VED.hxx:302-378) into the solver's fp64 SoA tensor

@@ -26,7 +26,7 @@ class VED:
                  scales=(0.300, 0.482, 0.775, 1.245, 2.000), iterations=1,
                  diffusion_iterations=5, cycle=C.VCYCLE, time_step=0.1, tolerance=1e-6,
                  diffusion_iterations_per_grid=2, verbose=False, smoother=C.GAUSS_SEIDEL,
-                 precision=C.FP32, device=-1, nranks=1, rank=0):
+                 precision=C.FP32, device=-1, nranks=1, rank=0, hessian="recursive"):
         if len(shape) != 3:
             raise ValueError("VED is 3D (itkVEDMultigridImageFilter.h:46)")
         if len(scales) > C.VED_MAX_SCALES:
@@ -50,6 +50,9 @@ class VED:
         d.verbose = int(bool(verbose))
         d.smoother, d.precision, d.device = int(smoother), int(precision), int(device)
         d.nranks, d.rank = int(nranks), int(rank)
+        # ComputeHessian operator: "recursive" (ITK's HessianRecursiveGaussianImageFilter, the
+        # reference's, default) or "fir" (sampled Gaussian derivative taps)
+        d.hessian = {"recursive": C.VED_HESSIAN_RECURSIVE, "fir": C.VED_HESSIAN_FIR}[hessian]
         self.desc = d
         self.nranks, self.rank = int(nranks), int(rank)
         nz = self.shape[0]
@@ -127,9 +130,10 @@ class VEDMultigridImageFilter:
     VCYCLE, FMG, SMOOTHER = C.VCYCLE, C.FMG, C.SMOOTHER
 
     def __init__(self, smoother=MultigridGaussSeidelSmoother, output_dtype=None,
-                 precision=C.FP32, device=-1):
+                 precision=C.FP32, device=-1, hessian="recursive"):
         self._smoother = smoother
         self._output_dtype = output_dtype
+        self._hessian = hessian
         self._precision = precision
         self._device = device
         self._p = dict(alpha=0.5, beta=0.5, gamma=5.0, epsilon=0.01, omega=5.0, sensitivity=10.0,
@@ -173,7 +177,7 @@ class VEDMultigridImageFilter:
         img = self._input
         out_dtype = self._output_dtype or img.array.dtype
         v = VED(img.array.shape, img.spacing, smoother=self._smoother.smoother_id,
-                precision=self._precision, device=self._device, **self._p)
+                precision=self._precision, device=self._device, hessian=self._hessian, **self._p)
         try:
             out, stats = v.run(img.array, out_dtype=out_dtype)
         finally:

@@ -52,17 +52,42 @@ def relmax(a, ref):
     return np.abs(a - ref).max() / np.abs(ref).max()
 
 
-@pytest.mark.parametrize("precision,tol", [("FP64", 1e-12), ("FP32", 2e-6)])
+@pytest.mark.parametrize("kind,precision,tol", [("recursive", "FP64", 1e-12), ("recursive", "FP32", 1e-12),
+                                                ("fir", "FP64", 1e-12), ("fir", "FP32", 2e-6)])
 @pytest.mark.parametrize("sigma", [0.3, 0.775, 2.0])
-def test_hessian_matches_oracle(M, precision, tol, sigma):
+def test_hessian_matches_oracle(M, kind, precision, tol, sigma):
+    """ComputeHessian (VED.hxx:158-173).  recursive (default): ITK's recursive Gaussian
+    operator, fp64 passes in both precision modes; fir: sampled taps in the storage type."""
     rng = np.random.default_rng(11)
     shape = (22, 26, 30)
     img = rng.normal(50.0, 20.0, size=shape)
-    v = M.VED(shape, SP, precision=getattr(M, precision))
+    v = M.VED(shape, SP, precision=getattr(M, precision), hessian=kind)
     H = v.hessian(img, sigma)
-    ref = VO.hessian(img, SP, sigma)
+    ref = VO.hessian(img, SP, sigma, kind)
     for q in range(6):
         assert relmax(H[q], ref[..., q]) < tol, q
+
+
+def test_recursive_hessian_on_four_point_axes(M):
+    """The recursive filter's shortest lines (4 points, ITK's minimum) and a long x axis."""
+    rng = np.random.default_rng(12)
+    for shape in [(4, 5, 6), (6, 4, 70)]:
+        img = rng.normal(50.0, 20.0, size=shape)
+        v = M.VED(shape, (0.7, 1.1, 0.9), precision=M.FP64)
+        H = v.hessian(img, 1.0)
+        ref = VO.hessian(img, (0.7, 1.1, 0.9), 1.0)
+        for q in range(6):
+            assert relmax(H[q], ref[..., q]) < 1e-12, (shape, q)
+
+
+def test_fir_hessian_filter_run_matches_oracle(M, oracle_mod):
+    """The round-1 operator stays selectable (hessian="fir") through the whole filter."""
+    crop = np.load(os.path.join(GOLDEN, "ved_crop_i16.npy"))
+    kw = dict(omega=1.5, diffusion_iterations=2, tolerance=1e-10, diffusion_iterations_per_grid=3)
+    v = M.VED(crop.shape, SP, precision=M.FP64, hessian="fir", **kw)
+    out, _ = v.run(crop, out_dtype=np.float64)
+    ref, _ = VO.ved_run(crop, SP, oracle_mod, hessian="fir", **kw)
+    assert relmax(out, ref) < 1e-8
 
 
 def test_tensor_matches_oracle_on_reference_crop(M):
