@@ -1964,12 +1964,13 @@ __global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fin
 // the grid) from a 4-slot LDS ring of u planes over that tile + 1 (x/y mirror images
 // in the ring, as resid3_k), the residuals go to an LDS tile, and restrict3_k's x-y
 // taps, z window and emission follow.  Residual arithmetic = resid3_k's, restriction
-// arithmetic = restrict3_k's, so b_c is bit-identical to residual + restriction.
+// arithmetic = restrict3_k's, so b_c is bit-identical to residual + restriction.  With zx
+// set, the coarse x is zeroed on the way (the descent's fill, MAD.hxx:415-416).
 // One rank (no ghost planes), nx, ny >= 3, nz >= 2.
 template <typename T, int KIND, int CX, int CY, int NT, bool BREC = false>
 __global__ void __launch_bounds__(NT) resid_restrict3_k(
     const T* __restrict__ u, const T* __restrict__ b, const T* __restrict__ cf, Geo gf, Rat<T> rat,
-    T* __restrict__ coarse, Geo gc, int cx, int cy, int cz, int kc, int ntx) {
+    T* __restrict__ coarse, T* __restrict__ zx, Geo gc, int cx, int cy, int cz, int kc, int ntx) {
   static_assert(CX * CY <= NT, "one coarse point per thread");
   constexpr int FX = 2 * CX + 2, FY = 2 * CY + 2, FP = FX * FY;  // residual tile
   constexpr int UX = FX + 2, UY = FY + 2, UP = UX * UY;          // u region (tile + 1)
@@ -2128,7 +2129,273 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
         T v = T(0);
 #pragma unroll
         for (int c = 0; c < 4; ++c) v = fma(wz[c], win[iz[c] & 3], v);
-        if (ok) coarse[I + gc.sy * J + gc.sz * (int64_t)K] = v;
+        if (ok) {
+          const int64_t o = I + gc.sy * J + gc.sz * (int64_t)K;
+          coarse[o] = v;
+          if (zx) zx[o] = T(0);
+        }
+        ++K;
+        if (K < K1) rtaps4<T>(K, gc.nz, cz, iz, wz);
+      }
+    }
+  }
+}
+
+// resid_restrict3g_k: resid_restrict3_k for the full 3D operator with g recomputed from
+// the 24-B tensor records (ct, pack_tensor_k) instead of read from the 36-B coefficient
+// records -- 24 + 4 (b) + 4 (u) bytes per fine voxel instead of 44.  The u region (the
+// residual tile + 1) is the unit of every load: per fine plane each thread loads its
+// region points' six tensor components; the in-plane ones (a_x a_y e_xy e_xz e_yz) go to
+// a two-slot LDS plane pair for the x / y differences, the z ones (a_z e_xz e_yz) into a
+// per-thread register window of planes f-1 .. f+1 for the z differences (the faces'
+// second planes f+2 / f-2 are loaded where they are needed).  g is gdelta / g_combine of the same values
+// build_g_k reads (neighbour planes clamped as there), so b_c is bit-identical to
+// resid_restrict3_k's.  u: a 3-slot LDS ring.  With zx set, the coarse x is zeroed on the
+// way (the descent's fill, MAD.hxx:415-416).  One rank, nx, ny >= 16, nz >= 2.
+template <typename T, int CX, int CY, int NT, int MINW = 1>
+__global__ void __launch_bounds__(NT, MINW) resid_restrict3g_k(
+    const T* __restrict__ u, const T* __restrict__ b, const T* __restrict__ ct, Geo gf,
+    T* __restrict__ coarse, T* __restrict__ zx, Geo gc, int cx, int cy, int cz, int kc, int ntx) {
+  static_assert(CX * CY <= NT, "one coarse point per thread");
+  constexpr int FX = 2 * CX + 2, FY = 2 * CY + 2, FP = FX * FY;  // residual tile
+  constexpr int UX = FX + 2, UY = FY + 2, UP = UX * UY;          // region (tile + 1)
+  constexpr int EPT = (UP + NT - 1) / NT;
+  constexpr uint32_t TS = sizeof(T);
+  __shared__ T ring[3 * UP];
+  __shared__ T tpl[2 * 5 * UP];
+  __shared__ T rt[FP];
+  const int tiles = ntx * ((gc.ny + CY - 1) / CY);
+  const int chunk = blockIdx.x / tiles;
+  const int t = blockIdx.x - chunk * tiles;
+  const int tyi = t / ntx, txi = t - (t / ntx) * ntx;
+  const int I0 = txi * CX, J0 = tyi * CY;
+  const int tid = threadIdx.x;
+  const int nx = gf.nx, ny = gf.ny, nz = gf.nz, sy = (int)gf.sy, hx0 = gf.hx0;
+  const int64_t sz = gf.sz;
+  const int fx0 = 2 * I0 - 1, fy0 = 2 * J0 - 1;
+  const int ux0 = fx0 - 1, uy0 = fy0 - 1;
+  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
+  const bool cthr = tid < CX * CY;
+  const int I = I0 + tid % CX, J = J0 + (tid / CX) % CY;
+  const bool ok = cthr && I < gc.nx && J < gc.ny;
+  // region points of this thread: mirrored sources (u dense, tensor record; a residual
+  // point lies in the domain, so its rhs offset is its u source offset) and rf = residual-
+  // tile index + 1 (0: not a residual point -- outside the tile or the domain, never
+  // tapped) << 4 | face flags (x lo / hi, y lo / hi as build_g_k sets them)
+  uint32_t u_src[EPT], t_src[EPT], rf[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int q = tid + e * NT;
+    const int qq = min(q, UP - 1);
+    const int lj = qq / UX, li = qq - (qq / UX) * UX;
+    const int xf = ux0 + li, yf = uy0 + lj;
+    const int xs = mirror(xf, nx), ys = mirror(yf, ny);
+    u_src[e] = (uint32_t)(ys * sy + xs) * TS;
+    t_src[e] = (uint32_t)(ys * sy + (xs & 1) * hx0 + (xs >> 1)) * (TS * 6);
+    const bool res = q < UP && li >= 1 && li <= FX && lj >= 1 && lj <= FY && xf >= 0 && xf < nx &&
+                     yf >= 0 && yf < ny;
+    const bool xl = xf == 0, xh = !xl && xf == nx - 1, yl = yf == 0, yh = !yl && yf == ny - 1;
+    rf[e] = (res ? (uint32_t)((lj - 1) * FX + li) << 4 : 0u) | (xl ? 1u : 0u) | (xh ? 2u : 0u) |
+            (yl ? 4u : 0u) | (yh ? 8u : 0u);
+  }
+  const int K0 = chunk * kc, K1 = min(K0 + kc, gc.nz);
+  int iz[4];
+  T wz[4];
+  rtaps4<T>(K0, gc.nz, cz, iz, wz);
+  const int f_lo = iz[0];
+  rtaps4<T>(K1 - 1, gc.nz, cz, iz, wz);
+  const int f_hi = max(max(iz[0], iz[1]), max(iz[2], iz[3]));
+
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+  auto wave_in = [&](int e) { return wbase + e * NT < UP; };
+  T up[EPT];
+  T P[EPT][6];     // tensor record of the plane in flight
+  T W[EPT][3][3];  // a_z e_xz e_yz of planes f-1 .. f+1 (after the push of f+1)
+  T bv[EPT];
+  auto uslot = [](int m) { return ring + ((unsigned)m % 3u) * UP; };
+  auto load_plane = [&](int m) {
+    m = min(max(m, 0), nz - 1);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (e == 0 || wave_in(e)) up[e] = buf_load<T>(rs, u_src[e], 0u);
+  };
+  auto put_plane = [&](int m) {
+    T* S = uslot(m);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (tid + e * NT < UP) S[tid + e * NT] = up[e];
+  };
+  auto load_t = [&](int m) {
+    m = min(max(m, 0), nz - 1);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(ct + (int64_t)m * sz * 6);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (e == 0 || wave_in(e)) buf_load_rec<T, 6>(rs, t_src[e], P[e]);
+  };
+  // plane m (in P) -> LDS slot m & 1 and the z window
+  auto push = [&](int m) {
+    T* S = tpl + (m & 1) * 5 * UP;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int q = tid + e * NT;
+      if (q < UP) {
+        S[q] = P[e][0];
+        S[UP + q] = P[e][1];
+        S[2 * UP + q] = P[e][3];
+        S[3 * UP + q] = P[e][4];
+        S[4 * UP + q] = P[e][5];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) W[e][s][c] = W[e][s + 1][c];
+      W[e][2][0] = P[e][2];
+      W[e][2][1] = P[e][4];
+      W[e][2][2] = P[e][5];
+    }
+  };
+  auto load_b = [&](int m) {
+    const __amdgpu_buffer_rsrc_t rb = buf_rsrc(b + (int64_t)m * sz);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (e == 0 || wave_in(e)) bv[e] = buf_load<T>(rb, u_src[e], 0u);
+  };
+
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) W[e][s][c] = T(0);
+  if (f_lo - 1 >= 0) {
+    load_plane(f_lo - 1);
+    put_plane(f_lo - 1);
+  }
+  load_plane(f_lo);
+  put_plane(f_lo);
+  load_plane(f_lo + 1);
+  load_t(f_lo - 1);
+  push(f_lo - 1);
+  load_t(f_lo);
+  push(f_lo);
+  load_t(f_lo + 1);  // pushed at the first step's top
+  load_b(f_lo);
+  T win[4];
+  int K = K0;
+  rtaps4<T>(K, gc.nz, cz, iz, wz);
+  for (int f = f_lo; f <= f_hi; ++f) {
+    if (f + 1 < nz) put_plane(f + 1);
+    push(f + 1);  // window: planes f-1 .. f+1
+    load_plane(f + 2);
+    __syncthreads();  // u planes f-1..f+1 and tensor plane f staged; last restriction done
+    const int zm = f == 0 ? f + 1 : f - 1;
+    const int zp = f == nz - 1 ? f - 1 : f + 1;
+    const bool zl = f == 0, zh = !zl && f == nz - 1;
+    const T* TP = tpl + (f & 1) * 5 * UP;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      if (e > 0 && !wave_in(e)) continue;
+      const uint32_t fe = rf[e];
+      if (fe < 16u) continue;
+      const int q = tid + e * NT;
+      const T* A = TP + q;
+      T dxax, dyay, dxexy, dyexy, dxexz, dyeyz;
+      if (fe & 15u) {  // x / y face point: the one-sided points (inside the region there)
+        const bool xl = fe & 1u, xh = fe & 2u, yl = fe & 4u, yh = fe & 8u;
+        const int xm2 = xh ? -2 : 0, xp2 = xl ? 2 : 0, ym2 = yh ? -2 * UX : 0, yp2 = yl ? 2 * UX : 0;
+        dxax = gdelta(A[xm2], A[-1], A[0], A[1], A[xp2], xl, xh);
+        dyay = gdelta(A[UP + ym2], A[UP - UX], A[UP], A[UP + UX], A[UP + yp2], yl, yh);
+        dxexy = gdelta(A[2 * UP + xm2], A[2 * UP - 1], A[2 * UP], A[2 * UP + 1], A[2 * UP + xp2], xl, xh);
+        dyexy = gdelta(A[2 * UP + ym2], A[2 * UP - UX], A[2 * UP], A[2 * UP + UX], A[2 * UP + yp2], yl, yh);
+        dxexz = gdelta(A[3 * UP + xm2], A[3 * UP - 1], A[3 * UP], A[3 * UP + 1], A[3 * UP + xp2], xl, xh);
+        dyeyz = gdelta(A[4 * UP + ym2], A[4 * UP - UX], A[4 * UP], A[4 * UP + UX], A[4 * UP + yp2], yl, yh);
+      } else {  // interior: central differences (gdelta's own interior branch)
+        dxax = gdelta(T(0), A[-1], T(0), A[1], T(0), false, false);
+        dyay = gdelta(T(0), A[UP - UX], T(0), A[UP + UX], T(0), false, false);
+        dxexy = gdelta(T(0), A[2 * UP - 1], T(0), A[2 * UP + 1], T(0), false, false);
+        dyexy = gdelta(T(0), A[2 * UP - UX], T(0), A[2 * UP + UX], T(0), false, false);
+        dxexz = gdelta(T(0), A[3 * UP - 1], T(0), A[3 * UP + 1], T(0), false, false);
+        dyeyz = gdelta(T(0), A[4 * UP - UX], T(0), A[4 * UP + UX], T(0), false, false);
+      }
+      // the faces' second planes f+2 / f-2 are loaded here (uniform: two planes only)
+      T z2[3] = {T(0), T(0), T(0)};
+      if (zl || zh) {
+        T r2[6];
+        buf_load_rec<T, 6>(buf_rsrc(ct + (int64_t)min(max(zl ? f + 2 : f - 2, 0), nz - 1) * sz * 6),
+                           t_src[e], r2);
+        z2[0] = r2[2];
+        z2[1] = r2[4];
+        z2[2] = r2[5];
+      }
+      const T dzaz = gdelta(z2[0], W[e][0][0], W[e][1][0], W[e][2][0], z2[0], zl, zh);
+      const T dzexz = gdelta(z2[1], W[e][0][1], W[e][1][1], W[e][2][1], z2[1], zl, zh);
+      const T dzeyz = gdelta(z2[2], W[e][0][2], W[e][1][2], W[e][2][2], z2[2], zl, zh);
+      Coefs<T> c;
+      g_combine<T, 3, KFULL>(dxax, dyay, dzaz, dxexy, dyexy, dxexz, dzexz, dyeyz, dzeyz, c.gx, c.gy, c.gz);
+      c.ax = A[0];
+      c.ay = A[UP];
+      c.az = W[e][1][0];
+      c.exy = A[2 * UP];
+      c.exz = A[3 * UP];
+      c.eyz = A[4 * UP];
+      const T* P0 = uslot(f) + q;
+      const T* Pm = uslot(zm) + q;
+      const T* Pp = uslot(zp) + q;
+      T nb[18];
+      nb[0] = P0[1];
+      nb[1] = P0[-1];
+      nb[2] = P0[UX];
+      nb[3] = P0[-UX];
+      nb[4] = Pp[0];
+      nb[5] = Pm[0];
+      nb[6] = P0[1 + UX];
+      nb[7] = P0[1 - UX];
+      nb[8] = P0[-1 + UX];
+      nb[9] = P0[-1 - UX];
+      nb[10] = Pp[1];
+      nb[11] = Pm[1];
+      nb[12] = Pp[-1];
+      nb[13] = Pm[-1];
+      nb[14] = Pp[UX];
+      nb[15] = Pm[UX];
+      nb[16] = Pp[-UX];
+      nb[17] = Pm[-UX];
+      T D, S;
+      stencil_combine<T, 3, KFULL>(c, nb, D, S);
+      rt[(fe >> 4) - 1] = resid_value(bv[e], D, P0[0], S);
+      __builtin_amdgcn_sched_barrier(0);  // one point at a time: registers are the limit
+    }
+    // next plane's tensor records and rhs: in flight across the restriction (P is dead
+    // during the point computation, which is where the registers peak)
+    load_t(f + 2);
+    if (f < f_hi) load_b(f + 1);
+    __syncthreads();  // residual tile of plane f complete
+    {
+#pragma clang fp contract(off)  // restrict3_k's explicit-fma order
+      int ix[4], iy[4];  // recomputed per plane: registers are the limit here
+      T wx[4], wy[4];
+      rtaps4<T>(min(I, gc.nx - 1), gc.nx, cx, ix, wx);
+      rtaps4<T>(min(J, gc.ny - 1), gc.ny, cy, iy, wy);
+      T vz = T(0);
+#pragma unroll
+      for (int bq = 0; bq < 4; ++bq) {
+        const T* row = rt + (iy[bq] - fy0) * FX - fx0;
+        T vy = T(0);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) vy = fma(wx[a], row[ix[a]], vy);
+        vz = fma(wy[bq], vy, vz);
+      }
+      win[f & 3] = vz;
+      while (K < K1 && max(max(iz[0], iz[1]), max(iz[2], iz[3])) == f) {
+        T v = T(0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v = fma(wz[c], win[iz[c] & 3], v);
+        if (ok) {
+          const int64_t o = I + gc.sy * J + gc.sz * (int64_t)K;
+          coarse[o] = v;
+          if (zx) zx[o] = T(0);
+        }
         ++K;
         if (K < K1) rtaps4<T>(K, gc.nz, cz, iz, wz);
       }

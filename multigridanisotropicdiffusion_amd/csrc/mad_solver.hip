@@ -362,7 +362,8 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * ctot));
       HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
-      if (dim == 3 && c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d)) {
+      if ((dim == 3 && c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d)) ||
+          (l + 1 < nl && rr_g_level(c, l, L))) {
         const int64_t tplane = L.g.sz * 6;
         const int64_t ttot = (L.g.nz + 2 * cgp) * tplane + 2 * margin * 6;
         HIP_CHECK(hipMalloc(&L.ct_alloc, sizeof(T) * ttot));
@@ -584,6 +585,25 @@ class Solver final : public SolverBase {
       return e && e[0] == '1';
     }();
     return v;
+  }
+  // V-cycle descent with g recomputed from the tensor records (resid_restrict3g_k: 32
+  // instead of 44 B per fine voxel): full 3D tensor, V-cycle / FMG solves, levels the
+  // one-pass residual + restriction runs on and whose records carry no b.  Opt-in
+  // (MAD_RR_G=1, measurement runs): bit-identical, but it issues 2.1x the VALU / LDS / SALU
+  // instructions of resid_restrict3_k and runs 1.2-1.5x slower at 512^3 (DESIGN.md,
+  // profiles/r02_rr_g_ab.md)
+  static bool rr_g_env() {
+    static const bool v = [] {
+      const char* e = std::getenv("MAD_RR_G");
+      return e && e[0] == '1';
+    }();
+    return v;
+  }
+  static bool rr_g_level(const mad_ctx* c, int l, const LevelData<T>& L) {
+    const LevelGeom& G = c->geom[l];
+    return rr_g_env() && c->dim == 3 && c->kind == KFULL && c->d.cycle != MAD_SMOOTHER && !L.brec &&
+           !G.distributed && !c->geom[l + 1].distributed && L.g.nx >= 16 && L.g.ny >= 16 &&
+           L.g.nz >= 2;
   }
   static bool fusedg_wanted(const mad_desc& d) {
     return d.gs_kernel == 5 || d.gs_kernel == 6 ||
@@ -1130,7 +1150,8 @@ class Solver final : public SolverBase {
   // rank (one GPU, or the replicated coarse levels); false: not applicable, the caller
   // runs residual + restriction.  MAD_FUSED_RR=0 turns it off (A/B runs).
   bool residual_restrict(int l) override { return resid_restrict(l); }
-  bool resid_restrict(int l) {
+  // zero_x: also zero x[l+1] (the V-cycle descent's fill, folded into the same pass)
+  bool resid_restrict(int l, bool zero_x = false) {
     static const bool on = [] {
       const char* e = std::getenv("MAD_FUSED_RR");
       return !(e && e[0] == '0');
@@ -1142,13 +1163,45 @@ class Solver final : public SolverBase {
       return false;
     sync_brec(l);
     C.b_halo_ok = C.brec_ok = false;
-    static const int tile = [] {
-      const char* e = std::getenv("MAD_RR_TILE");  // tuning runs only: 0 32x8, 1 32x16 coarse
-      return e ? std::atoi(e) : 0;
-    }();
+    T* zx = zero_x ? C.x : nullptr;
+    if (zero_x) x_changed(l + 1);
     static const int target = [] {
       const char* e = std::getenv("MAD_RR_BLOCKS");  // tuning runs only
       return e ? std::max(1, std::atoi(e)) : 1024;
+    }();
+    if (F.ct && !F.brec && c_->kind == KFULL && rr_g_env()) {
+      constexpr int CX = 32, CY = 8;
+      // MAD_RR_G_OCC (tuning runs): 1 caps registers at 128 for two 512-thread blocks per
+      // CU, 0 leaves them uncapped (one block per CU), 2: one 1024-thread block per CU
+      static const int occ = [] {
+        const char* e = std::getenv("MAD_RR_G_OCC");
+        return e ? std::atoi(e) : 1;
+      }();
+      const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
+      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / 4));
+      const int kc = (C.g.nz + chunks - 1) / chunks;
+      chunks = (C.g.nz + kc - 1) / kc;
+      const dim3 grid((unsigned)(ntx * nty * chunks));
+      auto go = [&](auto NTc, auto W) {
+        constexpr int NT = decltype(NTc)::value;
+        hipLaunchKernelGGL((resid_restrict3g_k<T, CX, CY, NT, decltype(W)::value>), grid, dim3(NT), 0,
+                           c_->stream, F.x, F.b, F.ct, F.g, C.b, zx, C.g, C.cent[0], C.cent[1],
+                           C.cent[2], kc, ntx);
+      };
+      using I512 = std::integral_constant<int, 512>;
+      if constexpr (sizeof(T) == 4) {
+        if (occ == 1) go(I512{}, std::integral_constant<int, 4>{});
+        else if (occ == 2) go(std::integral_constant<int, 1024>{}, std::integral_constant<int, 4>{});
+        else go(I512{}, std::integral_constant<int, 1>{});
+      } else {
+        go(I512{}, std::integral_constant<int, 1>{});  // 151 KB of LDS: one block per CU anyway
+      }
+      HIP_CHECK(hipGetLastError());
+      return true;
+    }
+    static const int tile = [] {
+      const char* e = std::getenv("MAD_RR_TILE");  // tuning runs only: 0 32x8, 1 32x16 coarse
+      return e ? std::atoi(e) : 0;
     }();
     // 512-thread blocks, two per CU (one block's barriers overlap the other's loads):
     // 1.133 vs 1.177 ms per 512^3 launch at 1024 blocks (profiles/r01_rr_nt_prof.log)
@@ -1167,11 +1220,12 @@ class Solver final : public SolverBase {
         constexpr int KD = decltype(K)::value;
         if (F.brec)
           hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT, true>), grid, block, 0, c_->stream,
-                             F.x, F.b, F.cf, F.g, F.rat, C.b, C.g, C.cent[0], C.cent[1], C.cent[2], kc,
-                             ntx);
+                             F.x, F.b, F.cf, F.g, F.rat, C.b, zx, C.g, C.cent[0], C.cent[1], C.cent[2],
+                             kc, ntx);
         else
           hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT>), grid, block, 0, c_->stream, F.x,
-                             F.b, F.cf, F.g, F.rat, C.b, C.g, C.cent[0], C.cent[1], C.cent[2], kc, ntx);
+                             F.b, F.cf, F.g, F.rat, C.b, zx, C.g, C.cent[0], C.cent[1], C.cent[2], kc,
+                             ntx);
       };
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
@@ -1269,11 +1323,11 @@ class Solver final : public SolverBase {
     } else {
       smooth(l, nu);  // MAD.hxx:384-411
     }
-    if (!resid_restrict(l)) {
+    if (!resid_restrict(l, true)) {  // x[l+1] zeroed in the same pass
       residual(l, false);  // MAD.hxx:389 (after the last pre-smoothing sweep)
       restrict_down(l);    // MAD.hxx:413
+      fill(l + 1, MAD_X, 0.0);  // MAD.hxx:415-416
     }
-    fill(l + 1, MAD_X, 0.0);  // MAD.hxx:415-416
     vcycle_rec(l + 1);        // MAD.hxx:418-420
     interpolate_up(l, true);  // MAD.hxx:422-435
     if (c_->d.verbose) verbose_line(l, 0, "initial");

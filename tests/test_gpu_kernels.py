@@ -240,6 +240,30 @@ def test_residual_restriction_one_pass_is_bitwise(shape, tensor, prec, cycle):
     """resid_restrict3_k (the V-cycle descent b_c = R (b - A x) without storing r) equals
     mad_residual + mad_restrict bit for bit on every level it applies to: partial tiles,
     odd (vertex-centred) and even (cell-centred) axes, chunked coarse planes."""
+    check_residual_restriction(shape, tensor, prec, cycle)
+
+
+def test_residual_restriction_in_kernel_g_is_bitwise():
+    """The opt-in descent with g recomputed from the tensor records (MAD_RR_G=1,
+    resid_restrict3g_k; measured slower) passes the same bitwise check on full
+    tensors in fp32 and fp64, in a child process (the switch is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import test_gpu_kernels as t\n"
+            "import multigridanisotropicdiffusion_amd as M\n"
+            "for p in (M.FP32, M.FP64):\n"
+            "    for sh in [(64, 64, 64), (40, 70, 130), (97, 33, 65), (130, 66, 24), (16, 17, 23)]:\n"
+            "        t.check_residual_restriction(sh, 'full', p, 0)\n"
+            "print('ok')\n") % here
+    env = dict(os.environ, MAD_RR_G="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def check_residual_restriction(shape, tensor, prec, cycle):
     import multigridanisotropicdiffusion_amd as M
     import synth
     T = {"full": lambda: synth.random_spd(shape, seed=1),
@@ -262,3 +286,28 @@ def test_residual_restriction_one_pass_is_bitwise(shape, tensor, prec, cycle):
         assert np.array_equal(got, ref), (l, np.abs(got - ref).max())
     if s.num_levels > 1 and min(s.shape_at(0)[1:]) >= 16:
         assert nfused >= 1
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 64), (40, 70, 130)])
+def test_vcycle_starts_coarse_levels_from_zero(shape, prec):
+    """The descent zeroes every coarse x before its smoothing (MAD.hxx:415-416): inside
+    resid_restrict3_k where the one-pass descent runs, by a fill elsewhere.  Garbage left in
+    the coarse x arrays does not change the V-cycle's result (bit for bit)."""
+    import multigridanisotropicdiffusion_amd as M
+    import synth
+    s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec)
+    s.set_tensor(synth.random_spd(shape, seed=1))
+    s.setup()
+    rng = np.random.default_rng(8)
+    x, b = rng.standard_normal(shape), rng.standard_normal(shape)
+    out = []
+    for fillv in (None, 0.0):
+        for l in range(1, s.num_levels):
+            sh = s.shape_at(l)
+            s.upload(l, M.capi.X, rng.standard_normal(sh) * 1e3 if fillv is None else np.zeros(sh))
+        s.upload(0, M.capi.X, x)
+        s.upload(0, M.capi.B, b)
+        s.vcycle()
+        out.append(s.download(0, M.capi.X))
+    s.close()
+    assert np.array_equal(out[0], out[1])

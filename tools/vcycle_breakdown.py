@@ -19,12 +19,11 @@ def main():
         grid = r.get("Grid_Size") or r.get("Grid_Size_X") or "?"
         ev.append((t0, t1, name, grid))
     ev.sort()
-    # the timed cycles are the last `cycles` repetitions: find the last gs_fused3 level-0
-    # pre-smoothing launch count: split at the largest grid fused launches (4 per cycle)
-    big = [i for i, e in enumerate(ev) if "gs_fused3_k" in e[2] and "true" in e[2]]
-    per = 4
-    start = big[-per * a.cycles]
-    sel = ev[start:]
+    # the timed cycles are the last `cycles` repetitions; one coarse solve per V-cycle, so the
+    # kernels after the (cycles+1)-th last coarse solve up to the last one are `cycles` whole
+    # cycles' worth (second half of one, first half of the next)
+    cs = [i for i, e in enumerate(ev) if "coarse_solve" in e[2]]
+    sel = ev[cs[-(a.cycles + 1)] + 1: cs[-1] + 1]
     span = (sel[-1][1] - sel[0][0]) / 1e6
     busy = sum(e[1] - e[0] for e in sel) / 1e6
     print(f"launches per cycle {len(sel) / a.cycles:.1f}; span {span / a.cycles:.3f} ms/cycle, "
