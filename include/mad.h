@@ -98,7 +98,7 @@ typedef struct mad_desc {
   int32_t precision;             /* MAD_FP32 (default), MAD_FP64 storage + arithmetic, or
                                     MAD_FP32_REFINE (fp32 cycles, fp64 defect correction) */
   int32_t stall_guard;           /* 1: end a time step once relres stops improving (the fp32
-                                    floor); default 1 for FP32, 0 for FP64 */
+                                    floor); default 1 for FP32 / FP32_REFINE, 0 for FP64 */
   int32_t device;                /* HIP device ordinal, -1 = current device */
   int32_t tensor_kind;           /* mad_tensor_kind, default AUTO */
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
