@@ -6,6 +6,7 @@
 // Reference: include/itkVEDMultigridImageFilter.{h,hxx} (VED.h / VED.hxx).
 #include "../../include/mad_ved.h"
 #include "mad_ved_kernels.hpp"
+#include <type_traits>
 
 struct mad_ved_ctx {
   mad_ved_desc d{};
@@ -16,7 +17,7 @@ struct mad_ved_ctx {
   double* img = nullptr;   // internal image (fp64, VED.h:61)
   double* img2 = nullptr;  // next iterate
   void* fir = nullptr;     // 9 FIR volumes in the storage precision
-  double* iir = nullptr;   // 12 fp64 volumes of the recursive Hessian passes
+  double* iir = nullptr;   // 12 volumes (T) of the recursive Hessian passes
   void* taps = nullptr;    // per-axis taps of the current scale (device)
   double* resp = nullptr;  // m_MaxVesselnessResponse
   double* dir = nullptr;   // vessel direction (eigenvector column 2 of the max scale), SoA x3
@@ -223,18 +224,74 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
           "the recursive Gaussian needs at least 4 points along each axis");
   const int64_t N = v->N;
   if (!v->iir) HIP_CHECK(hipMalloc(&v->iir, sizeof(double) * 12 * N));
+  // volumes between the passes in T: fp64 in the fp64 mode; fp32 in the fp32 mode (the
+  // passes' arithmetic stays fp64; half the bytes of the memory-bound passes)
+  T* base = reinterpret_cast<T*>(v->iir);
   // slots: Z 0..2, pairs A 6..11, Hessian 0..5 (over the dead Z: one SoA block)
-  double* Z[3] = {v->iir, v->iir + N, v->iir + 2 * N};
-  double* A[6];
-  double* H[6];
+  T* Z[3] = {base, base + N, base + 2 * N};
+  T* A[6];
+  T* H[6];
   for (int q = 0; q < 6; ++q) {
-    A[q] = v->iir + (6 + q) * N;
-    H[q] = v->iir + q * N;
+    A[q] = base + (6 + q) * N;
+    H[q] = base + q * N;
   }
   const double* h = v->d.spacing;
-  auto launch = [&](const IirPass& P, int axis) {
+  // MAD_VED_IIR_LINE=1 (A/B runs): ved_iir_k's one thread per line for every axis, each
+  // output marched on its own
+  static const bool line_walk = [] {
+    const char* e = std::getenv("MAD_VED_IIR_LINE");
+    return e && e[0] == '1';
+  }();
+  // SI: the z pass reads the fp64 image, the others the T volumes
+  auto launch = [&](const IirPass& P, int axis, auto si) {
+    using SI = decltype(si);
     const int64_t lines = axis == 0 ? (int64_t)ny * nz : axis == 1 ? (int64_t)nx * nz : (int64_t)nx * ny;
-    hipLaunchKernelGGL(ved_iir_k, dim3((unsigned)((lines + 255) / 256)), dim3(256), 0, st, P, axis, nx, ny, nz);
+    if (line_walk) {
+      hipLaunchKernelGGL((ved_iir_k<SI, T>), dim3((unsigned)((lines + 255) / 256)), dim3(256), 0, st, P, axis,
+                         nx, ny, nz);
+    } else if (axis == 0) {
+      // contiguous lines: one wave per 64 lines and output, LDS-staged row chunks
+      // chunk rows of one 128-B line (3.76 vs 4.15 ms per 512^3 fp32 pass with 64 B;
+      // MAD_VED_IIR_XC=0 for 64 B, measurement runs)
+      static const int wide = [] {
+        const char* e = std::getenv("MAD_VED_IIR_XC");
+        return e ? std::atoi(e) : 1;
+      }();
+      if constexpr (std::is_same<SI, T>::value) {
+        const dim3 gr((unsigned)((lines + 63) / 64), (unsigned)P.nout);
+        if (wide == 1)
+          hipLaunchKernelGGL((ved_iir_x_k<SI, T, 128 / (int)sizeof(T)>), gr, dim3(64), 0, st, P, nx, lines);
+        else
+          hipLaunchKernelGGL((ved_iir_x_k<SI, T, 64 / (int)sizeof(T)>), gr, dim3(64), 0, st, P, nx, lines);
+      }
+    } else {
+      // strided lines: the outputs sharing an input in one march, one launch per input
+      const unsigned nb = (unsigned)((lines + 255) / 256);
+      bool done[6] = {false, false, false, false, false, false};
+      for (int o = 0; o < P.nout; ++o) {
+        if (done[o]) continue;
+        int outs[3], k = 0;
+        for (int o2 = o; o2 < P.nout && k < 3; ++o2)
+          if (!done[o2] && P.src[o2] == P.src[o]) {
+            outs[k++] = o2;
+            done[o2] = true;
+          }
+        auto go = [&](auto KC) {
+          constexpr int K = decltype(KC)::value;
+          IirGroup<K> G{};
+          G.in = P.in[P.src[o]];
+          for (int q = 0; q < K; ++q) {
+            G.out[q] = P.out[outs[q]];
+            G.c[q] = P.c[outs[q]];
+            G.scale[q] = P.scale[outs[q]];
+          }
+          hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz);
+        };
+        if (k == 3) go(std::integral_constant<int, 3>{});
+        else if (k == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 1>{});
+      }
+    }
     HIP_CHECK(hipGetLastError());
   };
   IirPass P{};
@@ -247,7 +304,7 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     P.c[o] = ved_iir_coef(sigma / h[2], o);
     P.scale[o] = 1.0;
   }
-  launch(P, 2);
+  launch(P, 2, double{});
   // y: (oy, oz) = (0,0) (1,0) (2,0) (0,1) (1,1) (0,2)
   const int pairs[6][2] = {{0, 0}, {1, 0}, {2, 0}, {0, 1}, {1, 1}, {0, 2}};
   P = IirPass{};
@@ -259,7 +316,7 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     P.c[q] = ved_iir_coef(sigma / h[1], pairs[q][0]);
     P.scale[q] = 1.0;
   }
-  launch(P, 1);
+  launch(P, 1, T{});
   // x: H = [xx, xy, xz, yy, yz, zz] from (ox, pair) and sigma^2 / (h_i h_j)
   const int xsrc[6] = {0, 1, 3, 2, 4, 5};  // pair index feeding each component
   const int xord[6] = {2, 1, 1, 0, 0, 0};
@@ -274,15 +331,15 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     P.c[q] = ved_iir_coef(sigma / h[0], xord[q]);
     P.scale[q] = s2 / (h[cd[q][0]] * h[cd[q][1]]);
   }
-  launch(P, 0);
-  const double* Hs = H[0];
+  launch(P, 0, T{});
+  const T* Hs = H[0];
   const VesselParams vp{v->d.alpha, v->d.beta, v->d.gamma};
   const unsigned nb = flat_blocks(N);
   if (mode == VED_HESSIAN)
-    hipLaunchKernelGGL((ved_hess_k<T, VED_HESSIAN>), dim3(nb), dim3(256), 0, st, Hs, N, hess, nullptr,
+    hipLaunchKernelGGL((ved_hess_k<T, VED_HESSIAN, T>), dim3(nb), dim3(256), 0, st, Hs, N, hess, nullptr,
                        nullptr, 0, vp);
   else
-    hipLaunchKernelGGL((ved_hess_k<T, VED_UPDATE>), dim3(nb), dim3(256), 0, st, Hs, N, nullptr, v->resp,
+    hipLaunchKernelGGL((ved_hess_k<T, VED_UPDATE, T>), dim3(nb), dim3(256), 0, st, Hs, N, nullptr, v->resp,
                        v->dir, first ? 1 : 0, vp);
   HIP_CHECK(hipGetLastError());
 }

@@ -440,20 +440,23 @@ __device__ __forceinline__ void ved_point(double H0, double H1, double H2, doubl
 // host, ved_iir_coef in mad_ved.hpp, restating oracle/ved_oracle.py recursive_coefficients).
 // One thread per line: a causal pass (initial state: the first value extends to -infinity)
 // writes the output, an anticausal pass (last value to +infinity) adds its part, then the
-// output is scaled (x pass: sigma^2 / (h_i h_j)).  fp64 throughout (ITK's RealType), the
-// arithmetic in the oracle's order with contraction off.
+// output is scaled (x pass: sigma^2 / (h_i h_j)).  Arithmetic in fp64 (ITK's RealType), in
+// the oracle's order with contraction off; the volumes between passes are stored as SI / SO
+// (fp64 in the fp64 mode, fp32 in the fp32 mode, where the causal part is rounded once
+// before the anticausal part is added).
 struct IirCoef {
   double n[4], m[4], d[4], bn[4], bm[4];
 };
 struct IirPass {
-  const double* in[6];
-  double* out[6];
+  const void* in[6];  // SI (kernel template argument) volumes
+  void* out[6];       // SO volumes
   int src[6];       // input of each output
   IirCoef c[6];     // its filter along this pass's axis
   double scale[6];  // applied to the finished output
   int nout;
 };
 
+template <typename SI, typename SO>
 __global__ void __launch_bounds__(256) ved_iir_k(IirPass P, int axis, int nx, int ny, int nz) {
 #pragma clang fp contract(off)
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -477,8 +480,8 @@ __global__ void __launch_bounds__(256) ved_iir_k(IirPass P, int axis, int nx, in
     n = nz;
   }
   for (int o = 0; o < P.nout; ++o) {
-    const double* x = P.in[P.src[o]] + base;
-    double* y = P.out[o] + base;
+    const SI* x = static_cast<const SI*>(P.in[P.src[o]]) + base;
+    SO* y = static_cast<SO*>(P.out[o]) + base;
     const IirCoef& c = P.c[o];
     const double N0 = c.n[0], N1 = c.n[1], N2 = c.n[2], N3 = c.n[3];
     const double D1 = c.d[0], D2 = c.d[1], D3 = c.d[2], D4 = c.d[3];
@@ -521,7 +524,7 @@ __global__ void __launch_bounds__(256) ved_iir_k(IirPass P, int axis, int nx, in
       a2 -= a1 * D1 + v * c.bm[1] + v * c.bm[2] + v * c.bm[3];
       a3 -= a2 * D1 + a1 * D2 + v * c.bm[2] + v * c.bm[3];
       a4 -= a3 * D1 + a2 * D2 + a1 * D3 + v * c.bm[3];
-      double* yp = y + (int64_t)(n - 1) * st;
+      SO* yp = y + (int64_t)(n - 1) * st;
       yp[0] = (yp[0] + a1) * sc;
       yp[-st] = (yp[-st] + a2) * sc;
       yp[-2 * st] = (yp[-2 * st] + a3) * sc;
@@ -532,7 +535,7 @@ __global__ void __launch_bounds__(256) ved_iir_k(IirPass P, int axis, int nx, in
       for (int i = n - 4; i > 0; --i) {
         double ai = w0 * M1 + w1 * M2 + w2 * M3 + w3 * M4;  // a[i-1]
         ai -= b0 * D1 + b1 * D2 + b2 * D3 + b3 * D4;
-        double* yi = y + (int64_t)(i - 1) * st;
+        SO* yi = y + (int64_t)(i - 1) * st;
         yi[0] = (yi[0] + ai) * sc;
         w3 = w2; w2 = w1; w1 = w0; w0 = x[(int64_t)(i - 1) * st];
         b3 = b2; b2 = b1; b1 = b0; b0 = ai;
@@ -541,9 +544,307 @@ __global__ void __launch_bounds__(256) ved_iir_k(IirPass P, int axis, int nx, in
   }
 }
 
+// ved_iir_k for the strided axes (z, y: consecutive threads take consecutive x, so every
+// access is a coalesced row) with the K outputs that share an input filtered in one march
+// (each input value read twice per group -- causal, anticausal -- instead of twice per
+// output), the loads of B points issued together (one memory latency per block, not per
+// point).  One launch per group; its filters are kernel arguments indexed at compile time.
+// Per output the same expressions in the same order as ved_iir_k (bit-identical).
+template <int K>
+struct IirGroup {
+  const void* in;
+  void* out[K];
+  IirCoef c[K];
+  double scale[K];
+};
+
+template <typename SI, typename SO, int K>
+__global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, int nx, int ny, int nz) {
+#pragma clang fp contract(off)
+  constexpr int B = 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t base, st;
+  int n;
+  if (axis == 1) {  // along y, one per (x, z)
+    if (t >= (int64_t)nx * nz) return;
+    const int64_t i = t % nx, k = t / nx;
+    base = k * nx * ny + i;
+    st = nx;
+    n = ny;
+  } else {  // along z, one per (x, y)
+    if (t >= (int64_t)nx * ny) return;
+    base = t;
+    st = (int64_t)nx * ny;
+    n = nz;
+  }
+  const SI* __restrict__ x = static_cast<const SI*>(G.in) + base;
+  SO* y[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) y[q] = static_cast<SO*>(G.out[q]) + base;
+  // causal
+  {
+    const double v = x[0], x1 = x[st], x2 = x[2 * st], x3 = x[3 * st];
+    double sm1[K], sm2[K], sm3[K], sm4[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const IirCoef& C = G.c[q];
+      const double N0 = C.n[0], N1 = C.n[1], N2 = C.n[2], N3 = C.n[3];
+      const double D1 = C.d[0], D2 = C.d[1], D3 = C.d[2];
+      double s0 = v * N0 + v * N1 + v * N2 + v * N3;
+      double s1 = x1 * N0 + v * N1 + v * N2 + v * N3;
+      double s2 = x2 * N0 + x1 * N1 + v * N2 + v * N3;
+      double s3 = x3 * N0 + x2 * N1 + x1 * N2 + v * N3;
+      s0 -= v * C.bn[0] + v * C.bn[1] + v * C.bn[2] + v * C.bn[3];
+      s1 -= s0 * D1 + v * C.bn[1] + v * C.bn[2] + v * C.bn[3];
+      s2 -= s1 * D1 + s0 * D2 + v * C.bn[2] + v * C.bn[3];
+      s3 -= s2 * D1 + s1 * D2 + s0 * D3 + v * C.bn[3];
+      y[q][0] = s0;
+      y[q][st] = s1;
+      y[q][2 * st] = s2;
+      y[q][3 * st] = s3;
+      sm1[q] = s3; sm2[q] = s2; sm3[q] = s1; sm4[q] = s0;
+    }
+    double xm1 = x3, xm2 = x2, xm3 = x1;
+    for (int i0 = 4; i0 < n; i0 += B) {
+      SI xb[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) xb[u] = (i0 + u < n) ? x[(int64_t)(i0 + u) * st] : SI(0);
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int i = i0 + u;
+        if (i >= n) break;
+        const double xi = xb[u];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          const IirCoef& C = G.c[q];
+          double si = xi * C.n[0] + xm1 * C.n[1] + xm2 * C.n[2] + xm3 * C.n[3];
+          si -= sm1[q] * C.d[0] + sm2[q] * C.d[1] + sm3[q] * C.d[2] + sm4[q] * C.d[3];
+          y[q][(int64_t)i * st] = si;
+          sm4[q] = sm3[q]; sm3[q] = sm2[q]; sm2[q] = sm1[q]; sm1[q] = si;
+        }
+        xm3 = xm2; xm2 = xm1; xm1 = xi;
+      }
+    }
+  }
+  // anticausal, added to the causal part, then scaled
+  {
+    const double v = x[(int64_t)(n - 1) * st];
+    const double xa = v, xb = x[(int64_t)(n - 2) * st], xc = x[(int64_t)(n - 3) * st];
+    double b0[K], b1[K], b2[K], b3[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const IirCoef& C = G.c[q];
+      const double M1 = C.m[0], M2 = C.m[1], M3 = C.m[2], M4 = C.m[3];
+      const double D1 = C.d[0], D2 = C.d[1], D3 = C.d[2];
+      const double sc = G.scale[q];
+      double a1 = v * M1 + v * M2 + v * M3 + v * M4;
+      double a2 = xa * M1 + v * M2 + v * M3 + v * M4;
+      double a3 = xb * M1 + xa * M2 + v * M3 + v * M4;
+      double a4 = xc * M1 + xb * M2 + xa * M3 + v * M4;
+      a1 -= v * C.bm[0] + v * C.bm[1] + v * C.bm[2] + v * C.bm[3];
+      a2 -= a1 * D1 + v * C.bm[1] + v * C.bm[2] + v * C.bm[3];
+      a3 -= a2 * D1 + a1 * D2 + v * C.bm[2] + v * C.bm[3];
+      a4 -= a3 * D1 + a2 * D2 + a1 * D3 + v * C.bm[3];
+      SO* yp = y[q] + (int64_t)(n - 1) * st;
+      yp[0] = (yp[0] + a1) * sc;
+      yp[-st] = (yp[-st] + a2) * sc;
+      yp[-2 * st] = (yp[-2 * st] + a3) * sc;
+      yp[-3 * st] = (yp[-3 * st] + a4) * sc;
+      b0[q] = a4; b1[q] = a3; b2[q] = a2; b3[q] = a1;
+    }
+    double w0 = x[(int64_t)(n - 4) * st], w1 = xc, w2 = xb, w3 = xa;
+    // blocks of B points downward from i = n-4 (point i-1 each step), loads first
+    for (int i0 = n - 4; i0 > 0; i0 -= B) {
+      SI xp[B];
+      SO yb[K][B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int i = i0 - u;
+        xp[u] = (i > 0) ? x[(int64_t)(i - 1) * st] : SI(0);
+#pragma unroll
+        for (int q = 0; q < K; ++q) yb[q][u] = (i > 0) ? y[q][(int64_t)(i - 1) * st] : SO(0);
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int i = i0 - u;
+        if (i <= 0) break;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          const IirCoef& C = G.c[q];
+          double ai = w0 * C.m[0] + w1 * C.m[1] + w2 * C.m[2] + w3 * C.m[3];
+          ai -= b0[q] * C.d[0] + b1[q] * C.d[1] + b2[q] * C.d[2] + b3[q] * C.d[3];
+          y[q][(int64_t)(i - 1) * st] = (yb[q][u] + ai) * G.scale[q];
+          b3[q] = b2[q]; b2[q] = b1[q]; b1[q] = b0[q]; b0[q] = ai;
+        }
+        w3 = w2; w2 = w1; w1 = w0; w0 = xp[u];
+      }
+    }
+  }
+}
+
+// The x-axis pass of ved_iir_k with coalesced memory access.  Lines along x are contiguous
+// rows, so one thread per line reads 64 different rows per instruction; here one wave
+// takes 64 consecutive lines and one output, and every chunk of C points goes through an
+// LDS tile [64 lines][C] (+1 pad; one tile, reused for x and y): rows are loaded / stored by the whole wave (C doubles
+// per row, contiguous), each lane then runs its line's recursion on the tile.  Same
+// recursion, same expressions in the same order as ved_iir_k (bit-identical): the causal
+// and anticausal passes are written as per-point state machines over a sliding window,
+// with the first four points of each direction taking ved_iir_k's edge formulas.
+template <typename SI, typename SO, int C = 128 / (int)sizeof(SO)>
+__global__ void __launch_bounds__(64) ved_iir_x_k(IirPass P, int nx, int64_t nlines) {
+#pragma clang fp contract(off)
+  static_assert(sizeof(SI) == sizeof(SO), "the x pass reads and writes the volumes' storage type");
+  static_assert(64 % C == 0, "whole rows per wave instruction");
+  // tiles of the storage type (x chunk, y chunk), C values per row: LDS per wave bounds the
+  // waves per CU; a chunk of half a 128-B line leaves the other half to a later chunk
+  __shared__ SO tx[64 * (C + 1)];
+  __shared__ SO ty[64 * (C + 1)];
+  constexpr int RPI = 64 / C;  // rows per wave instruction
+  const int o = blockIdx.y;
+  const int lane = threadIdx.x;
+  const int64_t line0 = (int64_t)blockIdx.x * 64;
+  const SI* __restrict__ x = static_cast<const SI*>(P.in[P.src[o]]);
+  SO* __restrict__ y = static_cast<SO*>(P.out[o]);
+  const IirCoef c = P.c[o];
+  const double sc = P.scale[o];
+  const int n = nx;
+  // wave-cooperative row transfers of the chunk [i0, i0 + cnt) of lines line0 .. line0+63:
+  // instruction q moves rows RPI q + lrow, column lcol (all loads of a chunk in flight
+  // together, then the LDS writes).  Buffer accesses over the block's lines (record range),
+  // per-lane byte offsets; rows past the volume are masked (loads give 0, no stores).
+  const int lrow = lane / C, lcol = lane % C;
+  const int64_t nl = min((int64_t)64, nlines - line0);
+  const uint32_t nbytes = (uint32_t)(nl * n * (int64_t)sizeof(SO));
+  const uint32_t lofs = (uint32_t)((lrow * n + lcol) * (int)sizeof(SO));
+  const uint32_t qstep = (uint32_t)(RPI * n * (int)sizeof(SO));
+  auto rsrc = [&](const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
+  };
+  auto load_tile = [&](const SO* __restrict__ src, SO* t, int i0, int cnt) {
+    const auto r = rsrc(src + line0 * n);
+    const uint32_t off = lofs + (uint32_t)(i0 * (int)sizeof(SO));
+    SO v[C];
+#pragma unroll
+    for (int q = 0; q < C; ++q) {
+      v[q] = SO(0);
+      if (RPI * q + lrow < nl) {
+        const int vo = (int)(off + (uint32_t)q * qstep);
+        if constexpr (sizeof(SO) == 4)
+          v[q] = __builtin_bit_cast(SO, __builtin_amdgcn_raw_buffer_load_b32(r, vo, 0, 0));
+        else
+          v[q] = __builtin_bit_cast(SO, __builtin_amdgcn_raw_buffer_load_b64(r, vo, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < C; ++q) t[(RPI * q + lrow) * (C + 1) + lcol] = v[q];
+  };
+  auto store_tile = [&](SO* __restrict__ dst, const SO* t, int i0, int cnt) {
+    const auto r = rsrc(dst + line0 * n);
+    const uint32_t off = lofs + (uint32_t)(i0 * (int)sizeof(SO));
+    if (lcol >= cnt) return;
+#pragma unroll
+    for (int q = 0; q < C; ++q) {
+      if (RPI * q + lrow >= nl) continue;
+      const SO w = t[(RPI * q + lrow) * (C + 1) + lcol];
+      const int vo = (int)(off + (uint32_t)q * qstep);
+      if constexpr (sizeof(SO) == 4) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, w), r, vo, 0, 0);
+      } else {
+        using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, w), r, vo, 0, 0);
+      }
+    }
+  };
+  SO* mx = tx + lane * (C + 1);
+  SO* my = ty + lane * (C + 1);
+  const double N0 = c.n[0], N1 = c.n[1], N2 = c.n[2], N3 = c.n[3];
+  const double D1 = c.d[0], D2 = c.d[1], D3 = c.d[2], D4 = c.d[3];
+  // ---- causal: s[i] into y
+  double v = 0.0, x1 = 0.0, x2 = 0.0;                        // x[0], x[1], x[2] (edge formulas)
+  double xm1 = 0.0, xm2 = 0.0, xm3 = 0.0;                    // x[i-1], x[i-2], x[i-3]
+  double sm1 = 0.0, sm2 = 0.0, sm3 = 0.0, sm4 = 0.0;         // s[i-1] .. s[i-4]
+  for (int i0 = 0; i0 < n; i0 += C) {
+    const int cnt = min(C, n - i0);
+    load_tile(x, tx, i0, cnt);
+    __syncthreads();
+    for (int j = 0; j < cnt; ++j) {
+      const int i = i0 + j;
+      const double xi = mx[j];
+      double si;
+      if (i == 0) {
+        v = xi;
+        si = v * N0 + v * N1 + v * N2 + v * N3;
+        si -= v * c.bn[0] + v * c.bn[1] + v * c.bn[2] + v * c.bn[3];
+      } else if (i == 1) {
+        x1 = xi;
+        si = x1 * N0 + v * N1 + v * N2 + v * N3;
+        si -= sm1 * D1 + v * c.bn[1] + v * c.bn[2] + v * c.bn[3];
+      } else if (i == 2) {
+        x2 = xi;
+        si = x2 * N0 + x1 * N1 + v * N2 + v * N3;
+        si -= sm1 * D1 + sm2 * D2 + v * c.bn[2] + v * c.bn[3];
+      } else if (i == 3) {
+        si = xi * N0 + x2 * N1 + x1 * N2 + v * N3;
+        si -= sm1 * D1 + sm2 * D2 + sm3 * D3 + v * c.bn[3];
+      } else {
+        si = xi * N0 + xm1 * N1 + xm2 * N2 + xm3 * N3;
+        si -= sm1 * D1 + sm2 * D2 + sm3 * D3 + sm4 * D4;
+      }
+      mx[j] = si;  // in place: x[i] is consumed
+      xm3 = xm2; xm2 = xm1; xm1 = xi;
+      sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = si;
+    }
+    __syncthreads();
+    store_tile(y, tx, i0, cnt);
+    __syncthreads();
+  }
+  // ---- anticausal: a[k] from x[k+1 ..] and a[k+1 ..], y[k] = (s[k] + a[k]) * sc
+  const double M1 = c.m[0], M2 = c.m[1], M3 = c.m[2], M4 = c.m[3];
+  double V = 0.0, xa = 0.0, xb = 0.0;                        // x[n-1], x[n-1], x[n-2] (edge)
+  double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0;             // x[k+1] .. x[k+4]
+  double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;             // a[k+1] .. a[k+4]
+  const int nch = (n + C - 1) / C;
+  for (int ch = nch - 1; ch >= 0; --ch) {
+    const int i0 = ch * C, cnt = min(C, n - i0);
+    load_tile(x, tx, i0, cnt);
+    load_tile(y, ty, i0, cnt);
+    __syncthreads();
+    for (int j = cnt - 1; j >= 0; --j) {
+      const int k = i0 + j, m = n - 1 - k;
+      const double xk = mx[j];
+      double ak;
+      if (m == 0) {
+        V = xk;
+        xa = xk;
+        ak = V * M1 + V * M2 + V * M3 + V * M4;
+        ak -= V * c.bm[0] + V * c.bm[1] + V * c.bm[2] + V * c.bm[3];
+      } else if (m == 1) {
+        ak = xa * M1 + V * M2 + V * M3 + V * M4;
+        ak -= b0 * D1 + V * c.bm[1] + V * c.bm[2] + V * c.bm[3];
+        xb = xk;
+      } else if (m == 2) {
+        ak = xb * M1 + xa * M2 + V * M3 + V * M4;
+        ak -= b0 * D1 + b1 * D2 + V * c.bm[2] + V * c.bm[3];
+      } else if (m == 3) {
+        ak = w0 * M1 + xb * M2 + xa * M3 + V * M4;
+        ak -= b0 * D1 + b1 * D2 + b2 * D3 + V * c.bm[3];
+      } else {
+        ak = w0 * M1 + w1 * M2 + w2 * M3 + w3 * M4;
+        ak -= b0 * D1 + b1 * D2 + b2 * D3 + b3 * D4;
+      }
+      my[j] = (my[j] + ak) * sc;
+      w3 = w2; w2 = w1; w1 = w0; w0 = xk;
+      b3 = b2; b2 = b1; b1 = b0; b0 = ak;
+    }
+    __syncthreads();
+    store_tile(y, ty, i0, cnt);
+    __syncthreads();
+  }
+}
+
 // UpdateVesselness / Hessian output from the six recursive-Hessian volumes
-template <typename T, int MODE>
-__global__ void __launch_bounds__(256) ved_hess_k(const double* __restrict__ H, int64_t n,
+template <typename T, int MODE, typename S = double>
+__global__ void __launch_bounds__(256) ved_hess_k(const S* __restrict__ H, int64_t n,
                                                   double* __restrict__ hess, double* __restrict__ resp,
                                                   double* __restrict__ dir, int first, VesselParams vp) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
