@@ -239,6 +239,12 @@ int mad_comm_init(mad_ctx *ctx, const void *uid128);
  * ghost planes by device-to-device copies.  Same bytes as the RCCL path; used to
  * test the z-slab decomposition on a single GPU. */
 int mad_comm_init_local(mad_ctx *ctx, uint64_t group);
+/* Measurement only: this context runs as rank desc.rank of desc.nranks ALONE on its
+ * device.  Every exchange becomes a device copy of the same bytes within its own arrays
+ * (and the norm allreduce a no-op), so one rank's device time per sweep / V-cycle --
+ * graph replay, boundary + interior launches, communication-stream overlap -- can be
+ * timed on a one-GPU machine.  The values it computes are not the solution. */
+int mad_comm_init_solo(mad_ctx *ctx);
 /* Transport self-test on one GPU: a single-rank RCCL communicator runs the halo
  * exchange (grouped ncclSend/ncclRecv, both neighbours = this rank), the fp64
  * allreduce and the slab allgather the solver uses, on `device`, first eagerly and

@@ -13,6 +13,12 @@
 //        barriers for ordering.  It exists so the decomposition (ghost planes,
 //        global colour parity, coarsening alignment, agglomeration) is testable
 //        bit-for-bit on a one-GPU machine; RCCL and LOCAL move the same bytes.
+// SOLO   measurement only: one rank of an N-rank decomposition alone on its device.
+//        Every exchange is a stream-ordered device copy of the same bytes within the
+//        rank's own arrays (its boundary planes into its ghost planes, its slab into every
+//        slot of a gather, the allreduce a no-op), so one rank's per-cycle device time --
+//        hipGraph replay, boundary / interior launches, comm-stream overlap -- is measurable
+//        on a one-GPU box.  The numbers it computes are not the decomposition's results.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -88,7 +94,7 @@ inline std::shared_ptr<LocalGroup> local_group(uint64_t key, int nranks) {
 
 class Comm {
  public:
-  enum Mode { NONE, RCCL, LOCAL };
+  enum Mode { NONE, RCCL, LOCAL, SOLO };
 
   static void unique_id(void* out128) {
     ncclUniqueId id;
@@ -143,6 +149,14 @@ class Comm {
     group_->barrier();  // everyone joined
   }
 
+  void init_solo(int nranks, int rank) {
+    destroy();
+    if (nranks <= 1) return;
+    mode_ = SOLO;
+    nranks_ = nranks;
+    rank_ = rank;
+  }
+
   void destroy() {
     if (comm_) (void)ncclCommDestroy(comm_);
     comm_ = nullptr;
@@ -181,6 +195,14 @@ class Comm {
       NCCL_CHECK(ncclGroupEnd());
       return;
     }
+    if (mode_ == SOLO) {  // the same bytes, own boundary planes into own ghost planes
+      if (has_lo)
+        HIPC_CHECK(hipMemcpyAsync(base - depth * pb, base, depth * pb, hipMemcpyDeviceToDevice, s));
+      if (has_hi)
+        HIPC_CHECK(hipMemcpyAsync(base + (size_t)nz * pb, base + (size_t)(nz - depth) * pb, depth * pb,
+                                  hipMemcpyDeviceToDevice, s));
+      return;
+    }
     // LOCAL: publish, pull the neighbours' boundary planes, wait until all pulled
     HIPC_CHECK(hipStreamSynchronize(s));
     group_->ptr[rank_] = a;
@@ -203,6 +225,7 @@ class Comm {
       NCCL_CHECK(ncclAllReduce(p, p, n, ncclDouble, ncclSum, comm_, s));
       return;
     }
+    if (mode_ == SOLO) return;  // the rank's own partial stands for the sum
     if (n != 1) throw CommError("local allreduce supports one value");
     double v = 0.0;
     HIPC_CHECK(hipMemcpyAsync(&v, p, sizeof(double), hipMemcpyDeviceToHost, s));
@@ -229,7 +252,7 @@ class Comm {
       HIPC_CHECK(hipFree(d));
       return;
     }
-    if (mode_ != LOCAL) return;  // one rank: nothing to reduce
+    if (mode_ != LOCAL) return;  // one rank (or SOLO): nothing to reduce
     for (size_t q = 0; q < n; ++q) {
       group_->val[rank_] = v[q];
       group_->barrier();
@@ -246,6 +269,11 @@ class Comm {
     const size_t bytes = (size_t)plane * (size_t)(nz_global / nranks_) * esz;
     if (mode_ == RCCL) {
       NCCL_CHECK(ncclAllGather(slab, full, bytes / 4, ncclFloat, comm_, s));
+      return;
+    }
+    if (mode_ == SOLO) {  // the same bytes: the own slab into every rank's slot
+      for (int r = 0; r < nranks_; ++r)
+        HIPC_CHECK(hipMemcpyAsync((char*)full + r * bytes, slab, bytes, hipMemcpyDeviceToDevice, s));
       return;
     }
     HIPC_CHECK(hipStreamSynchronize(s));

@@ -228,11 +228,13 @@ __device__ __forceinline__ void stencil_terms(const T* __restrict__ u, const T* 
 //              2D colour = (i&1) | (j&1)<<1           (9-point)
 // Same-colour points are never neighbours, so a colour pass is order-free.
 // Thread (x, y, z) -> i' (half row), row index, plane.
+// kofs: first local plane of the launch (negative: ghost planes of a rank slab, computed
+// redundantly so that one deep halo exchange serves a whole sweep)
 template <typename T, int DIM, int KIND>
 __global__ void __launch_bounds__(256) gs_color_k(T* __restrict__ u, const T* __restrict__ b,
                                                   const T* __restrict__ cf, Geo g, Rat<T> rat,
-                                                  int color, int ncolors) {
-  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+                                                  int color, int ncolors, int kofs = 0) {
+  const int k = (DIM == 3) ? (int)blockIdx.z + kofs : 0;
   const int kg = k + g.zoff;
   const int jq = blockIdx.y * blockDim.y + threadIdx.y;
   const int iq = blockIdx.x * blockDim.x + threadIdx.x;

@@ -563,10 +563,11 @@ class Solver final : public SolverBase {
   struct ZRange {
     int zbase, zc, zstride, nchunks;
   };
-  // the whole slab in chunks sized for ~fc.blocks workgroups (at least 32 planes)
+  // the whole slab in chunks sized for ~fc.blocks workgroups (at least 16 planes: a
+  // 128-plane rank slab of a 256^2 level still fills the chip)
   static ZRange whole_range(int nz, int tiles, const FusedCfg& fc) {
     int chunks = (fc.blocks + tiles - 1) / tiles;
-    chunks = std::max(1, std::min(chunks, std::max(1, nz / 32)));
+    chunks = std::max(1, std::min(chunks, std::max(1, nz / 16)));
     const int zc = (nz + chunks - 1) / chunks;
     return ZRange{0, zc, zc, (nz + zc - 1) / zc};
   }
@@ -824,7 +825,7 @@ class Solver final : public SolverBase {
       std::snprintf(buf, sizeof buf, "gs_fusedg_k<%s, %d, %d, %d%s>", tn, tx, ty, nt,
                     (sizeof(T) == 4 && fusedg_tile() == 2) ? ", 2" : "");
       const LevelData<T>& L = lv_[l];
-      if (c_->comm.active() && c_->geom[l].distributed && L.g.nz >= 3 * boundary_planes()) {
+      if (sweep_overlap(l)) {
         int tiles = 0, nchunks = 0;
         fused_shape(L, &tiles, &nchunks);
         const bool single = L.sig && nchunks >= 2;
@@ -845,8 +846,7 @@ class Solver final : public SolverBase {
                     nt, sizeof(T) == 8 ? 2 : 4, lead, brec ? ", true" : "");
       // rank slabs: which sweep form fused_sweep takes
       const LevelData<T>& L = lv_[l];
-      if (c_->comm.active() && c_->geom[l].distributed && c_->d.gs_kernel != 2 &&
-          L.g.nz >= 3 * boundary_planes()) {
+      if (sweep_overlap(l)) {
         int tiles = 0, nchunks = 0;
         fused_shape(L, &tiles, &nchunks);
         const bool single = L.sig && nchunks >= 2;
@@ -877,6 +877,28 @@ class Solver final : public SolverBase {
     L.brec_ok = true;
   }
 
+  // Does the fused sweep of rank-slab level l overlap its halo exchange (boundary chunks
+  // first, the exchange beside the interior launch, or gs_kernel 4's single launch)?  The
+  // default form (gs_kernel 0) only where the boundary launch keeps half the chip busy
+  // (2 chunks x tiles per plane >= 128 workgroups): on smaller levels the split's short,
+  // under-filled boundary launch costs more than the exchange it hides (a 256^2-plane level
+  // at 2 ranks: 56 + 102 us per sweep split, profiles/r02_rank_vcycle.md), so they sweep in
+  // one launch and exchange afterwards.  MAD_SWEEP_OVERLAP=1 forces the split (A/B runs).
+  bool sweep_overlap(int l) const {
+    const LevelData<T>& L = lv_[l];
+    if (!(c_->comm.active() && c_->geom[l].distributed && c_->d.gs_kernel != 2 &&
+          L.g.nz >= 3 * boundary_planes()))
+      return false;
+    static const bool force = [] {
+      const char* e = std::getenv("MAD_SWEEP_OVERLAP");
+      return e && e[0] == '1';
+    }();
+    if (force || c_->d.gs_kernel != 0) return true;
+    int tiles = 0, nchunks = 0;
+    fused_shape(L, &tiles, &nchunks);
+    return 2 * tiles >= 128;
+  }
+
   // one fused GS sweep x -> t, then swap (gs_fused_k)
   // One fused GS sweep x -> t, then swap.  On a rank slab the halo exchange of the NEW
   // x is overlapped with the sweep: the two boundary chunks (which produce the planes
@@ -897,7 +919,7 @@ class Solver final : public SolverBase {
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
     const bool dist = c_->comm.active() && c_->geom[l].distributed;
-    const bool overlap = dist && c_->d.gs_kernel != 2 && L.g.nz >= 3 * boundary_planes();
+    const bool overlap = sweep_overlap(l);
     int tiles = 0, nchunks = 0;
     if (overlap) fused_shape(L, &tiles, &nchunks);
     if (overlap && L.sig && nchunks >= 2) {
@@ -985,6 +1007,17 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipGetLastError());
   }
 
+  // per-colour GS on a 3D rank slab with one halo exchange per sweep (MAD_COLOUR_CA=0:
+  // one exchange per colour, A/B runs)
+  bool colour_ca(int l) const {
+    static const bool env = [] {
+      const char* e = std::getenv("MAD_COLOUR_CA");
+      return !(e && e[0] == '0');
+    }();
+    return env && c_->dim == 3 && c_->comm.active() && c_->geom[l].distributed &&
+           c_->ncolors <= GHOST;
+  }
+
   void smooth(int l, unsigned n) override {
     LevelData<T>& L = lv_[l];
     const int dim = c_->dim;
@@ -1013,14 +1046,37 @@ class Solver final : public SolverBase {
       } else {
         const int nc = c_->ncolors;
         const int rows = (nc == 4) ? (L.g.ny + 1) / 2 : L.g.ny;
-        dim3 gr = grid_for((L.g.nx + 1) / 2, rows, L.g.nz, BLK);
-        for (int col = 0; col < nc; ++col) {
-          halo(l, L.x);
-          dispatch(dim, c_->kind, [&](auto D, auto K) {
-            hipLaunchKernelGGL((gs_color_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, L.x,
-                               L.b, L.cf, L.g, L.rat, col, nc);
-          });
+        if (colour_ca(l)) {
+          // rank slab: one exchange of nc ghost planes per sweep instead of one plane per
+          // colour; colour c is computed on the owned planes plus the nc - 1 - c nearest
+          // ghost planes (the values the neighbour computes, from the same inputs: the
+          // outermost of them reads ghost plane nc), so every later colour finds its ghost
+          // neighbours updated -- the fused sweep's scheme
+          halo(l, L.x, nc);
+          if (!L.b_halo_ok) {
+            halo(l, L.b, GHOST);
+            L.b_halo_ok = true;
+          }
+          for (int col = 0; col < nc; ++col) {
+            const int ext = nc - 1 - col;
+            const int k0 = L.g.zlo_ghost ? -ext : 0, k1 = L.g.nz + (L.g.zhi_ghost ? ext : 0);
+            dim3 gr = grid_for((L.g.nx + 1) / 2, rows, k1 - k0, BLK);
+            dispatch(dim, c_->kind, [&](auto D, auto K) {
+              hipLaunchKernelGGL((gs_color_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, L.x, L.b,
+                                 L.cf, L.g, L.rat, col, nc, k0);
+            });
+          }
           x_changed(l);
+        } else {
+          dim3 gr = grid_for((L.g.nx + 1) / 2, rows, L.g.nz, BLK);
+          for (int col = 0; col < nc; ++col) {
+            halo(l, L.x);
+            dispatch(dim, c_->kind, [&](auto D, auto K) {
+              hipLaunchKernelGGL((gs_color_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, L.x,
+                                 L.b, L.cf, L.g, L.rat, col, nc, 0);
+            });
+            x_changed(l);
+          }
         }
         HIP_CHECK(hipGetLastError());
       }
@@ -1406,7 +1462,8 @@ class Solver final : public SolverBase {
       const char* e = std::getenv("MAD_VGRAPH_RANKS");
       return !(e && e[0] == '0');
     }();
-    return env_ok && c_->comm.mode() == Comm::RCCL && c_->d.gs_kernel != 4 && c_->d.gs_kernel != 6;
+    return env_ok && (c_->comm.mode() == Comm::RCCL || c_->comm.mode() == Comm::SOLO) &&
+           c_->d.gs_kernel != 4 && c_->d.gs_kernel != 6;
   }
 
   struct HaloFlags {
@@ -2902,6 +2959,15 @@ int mad_comm_init_local(mad_ctx* c, uint64_t group) {
     REQUIRE(!c->setup_done, MAD_ERR_STATE, "mad_comm_init_local must precede mad_setup");
     use_device(c);
     c->comm.init_local(group, c->d.nranks, c->d.rank);
+  });
+}
+
+int mad_comm_init_solo(mad_ctx* c) {
+  if (!c) return MAD_ERR_INVALID;
+  return guarded(c, [&] {
+    REQUIRE(!c->setup_done, MAD_ERR_STATE, "mad_comm_init_solo must precede mad_setup");
+    use_device(c);
+    c->comm.init_solo(c->d.nranks, c->d.rank);
   });
 }
 

@@ -136,6 +136,11 @@ class Solver:
         """In-process transport: contexts sharing `group` exchange slabs directly."""
         self._check(self._L.mad_comm_init_local(self._ctx, int(group)))
 
+
+    def comm_init_solo(self):
+        """Measurement only (mad_comm_init_solo): this rank alone on its device, every
+        exchange a device copy of the same bytes; timings, not results."""
+        self._check(self._L.mad_comm_init_solo(self._ctx))
     def setup(self):
         self._check(self._L.mad_setup(self._ctx))
 

@@ -16,16 +16,28 @@ def main():
     p.add_argument("--layout", default="vcycle", choices=["vcycle", "smoother"],
                    help="solver CycleType: vcycle (production layout, dense rhs; bench.py's "
                         "V-cycles/s) or smoother (level-0 records carrying b)")
+    p.add_argument("--ranks", type=int, default=1,
+                   help="> 1: one interior rank (ranks // 2) of that z-slab decomposition alone "
+                        "on the device (mad_comm_init_solo; timings, not results)")
     a = p.parse_args()
     import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
     S = a.size
     cyc = M.VCYCLE if a.layout == "vcycle" else M.SMOOTHER
-    s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32, cycle=cyc)
+    if a.ranks > 1:
+        r = a.ranks // 2
+        z0, z1 = D.slabs((S, S, S), a.ranks)[r]
+        s = M.Solver((z1 - z0, S, S), time_step=0.1, precision=M.FP32, cycle=cyc, nranks=a.ranks,
+                     rank=r, global_shape=(S, S, S))
+        s.comm_init_solo()
+    else:
+        s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32, cycle=cyc)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
     s.synth_level(0, M.capi.X, 3)
     s.vcycle()
+    s.vcycle()  # (a rank slab's first cycle runs eagerly, the second is captured)
     s.synchronize()
     ms = s.bench_vcycle(a.cycles)
     print(f"ms_per_vcycle {ms / a.cycles:.3f}", flush=True)
