@@ -19,6 +19,8 @@ def main():
     p.add_argument("--ranks", type=int, default=1,
                    help="> 1: one interior rank (ranks // 2) of that z-slab decomposition alone "
                         "on the device (mad_comm_init_solo; timings, not results)")
+    p.add_argument("--sweeps", type=int, default=0,
+                   help="> 0: time that many level-0 sweeps instead of V-cycles")
     a = p.parse_args()
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
@@ -36,6 +38,11 @@ def main():
     s.setup()
     s.synth_level(0, M.capi.B, 3)
     s.synth_level(0, M.capi.X, 3)
+    if a.sweeps:
+        s.bench_smooth(0, 3)
+        dev, kern, nl = s.bench_smooth(0, a.sweeps)
+        print(f"ms_per_sweep {dev / a.sweeps:.4f} kernel_ms {kern:.4f} launches {nl}", flush=True)
+        return
     s.vcycle()
     s.vcycle()  # (a rank slab's first cycle runs eagerly, the second is captured)
     s.synchronize()
