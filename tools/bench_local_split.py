@@ -53,7 +53,7 @@ def solo(ns):
             s.close()
         if n == 1:
             ref = dict(out)
-        else:
+        elif ref:
             out["sweep_speedup_vs_1"] = ref["ms_per_sweep"] / out["ms_per_sweep"]
             out["vcycle_speedup_vs_1"] = ref["ms_per_vcycle"] / out["ms_per_vcycle"]
         print(json.dumps(out), flush=True)
