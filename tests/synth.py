@@ -106,3 +106,24 @@ def vesselness_field(x, y, z, shape, seed):
 def image(shape, seed=1):
     rng = np.random.default_rng(seed)
     return rng.uniform(0.0, 1.0, size=shape)
+
+
+def tube_phantom(S, seed=4):
+    """C4's VED input: bright axis-aligned tubes (radius 2..6 voxels, intensity
+    200 on 0) plus N(0, 10^2) noise, fp32 (z, y, x) -- the volume tools/bench_ved.py times."""
+    rng = np.random.default_rng(seed)
+    img = rng.normal(0.0, 10.0, size=(S, S, S)).astype(np.float32)
+    g = np.arange(S, dtype=np.float32)
+    for axis in range(3):
+        prof = np.zeros((S, S), np.float32)
+        for _ in range(64 // 3 + (1 if axis < 64 % 3 else 0)):
+            a, b = rng.uniform(8, S - 8, size=2)
+            r = rng.uniform(2, 6)
+            prof += 200.0 * np.exp(-((g[:, None] - a) ** 2 + (g[None, :] - b) ** 2) / (2 * r * r))
+        if axis == 0:
+            img += prof[None, :, :]
+        elif axis == 1:
+            img += prof[:, None, :]
+        else:
+            img += prof[:, :, None]
+    return img
