@@ -139,3 +139,30 @@ def test_rccl_transport_selftest():
     rc = L.mad_comm_selftest(0, ctypes.byref(err))
     assert rc == 0, L.mad_last_error(None)
     assert err.value == 0.0
+
+
+def test_solo_transport_times_one_rank():
+    """mad_comm_init_solo (measurement only): one interior rank of a 4-rank decomposition alone
+    on the device runs sweeps and graph-replayed V-cycles (every exchange a device copy of the
+    same bytes) -- the per-rank timing path of tools/bench_local_split.py --solo."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (128, 64, 64)
+    z0, z1 = D.slabs(shape, 4)[2]
+    for cyc in (M.SMOOTHER, M.VCYCLE):
+        s = M.Solver((z1 - z0,) + shape[1:], time_step=0.1, cycle=cyc, nranks=4, rank=2,
+                     global_shape=shape)
+        s.comm_init_solo()
+        s.set_tensor(synth.random_spd(shape, seed=9))
+        s.setup()
+        s.synth_level(0, M.capi.B, 3)
+        s.synth_level(0, M.capi.X, 3)
+        if cyc == M.SMOOTHER:
+            dev, kern, n = s.bench_smooth(0, 4)
+            assert dev > 0 and n >= 4
+        else:
+            s.vcycle()
+            s.vcycle()
+            assert s.bench_vcycle(3) > 0
+        assert np.isfinite(s.download(0, M.capi.X)).all()
+        s.close()
