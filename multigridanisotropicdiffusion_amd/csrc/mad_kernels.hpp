@@ -1968,11 +1968,15 @@ __global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fin
 // taps, z window and emission follow.  Residual arithmetic = resid3_k's, restriction
 // arithmetic = restrict3_k's, so b_c is bit-identical to residual + restriction.  With zx
 // set, the coarse x is zeroed on the way (the descent's fill, MAD.hxx:415-416).
-// One rank (no ghost planes), nx, ny >= 3, nz >= 2.
+// Rank slabs: the coarse planes' taps are taken in global indices (coarse zoff, global coarse
+// nz `ncz`) and shifted to local fine planes by fzs (the fine zoff); taps past the slab
+// residualise the fine ghost planes (u, b and records current there: >= 2 ghost planes), the
+// z mirror only at the global faces.  nx, ny >= 3, nz >= 2.
 template <typename T, int KIND, int CX, int CY, int NT, bool BREC = false>
 __global__ void __launch_bounds__(NT) resid_restrict3_k(
     const T* __restrict__ u, const T* __restrict__ b, const T* __restrict__ cf, Geo gf, Rat<T> rat,
-    T* __restrict__ coarse, T* __restrict__ zx, Geo gc, int cx, int cy, int cz, int kc, int ntx) {
+    T* __restrict__ coarse, T* __restrict__ zx, Geo gc, int cx, int cy, int cz, int kc, int ntx,
+    int fzs, int ncz) {
   static_assert(CX * CY <= NT, "one coarse point per thread");
   constexpr int FX = 2 * CX + 2, FY = 2 * CY + 2, FP = FX * FY;  // residual tile
   constexpr int UX = FX + 2, UY = FY + 2, UP = UX * UY;          // u region (tile + 1)
@@ -2027,16 +2031,24 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
   const int K0 = chunk * kc, K1 = min(K0 + kc, gc.nz);
   int iz[4];
   T wz[4];
-  rtaps4<T>(K0, gc.nz, cz, iz, wz);
+  // z taps of local coarse plane K as local fine planes
+  auto ztaps = [&](int Kl) {
+    rtaps4<T>(Kl + gc.zoff, ncz, cz, iz, wz);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) iz[c] -= fzs;
+  };
+  ztaps(K0);
   const int f_lo = iz[0];
-  rtaps4<T>(K1 - 1, gc.nz, cz, iz, wz);
+  ztaps(K1 - 1);
   const int f_hi = max(max(iz[0], iz[1]), max(iz[2], iz[3]));
+  // loadable planes: the slab plus 2 ghost planes where a neighbour rank has them
+  const int ulo = gf.zlo_ghost ? -2 : 0, uhi = gf.zhi_ghost ? nz + 2 : nz;
 
   T up[UPT];
   T raw[RPT][RS];
   T bv[RPT];
   auto load_plane = [&](int m) {
-    m = min(max(m, 0), nz - 1);
+    m = min(max(m, ulo), uhi - 1);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
 #pragma unroll
     for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src[e], 0u);
@@ -2051,7 +2063,7 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   auto wave_in = [&](int e) { return wbase + e * NT < FP; };
   auto load_pts = [&](int m) {
-    m = min(max(m, 0), nz - 1);
+    m = min(max(m, ulo), uhi - 1);
     const __amdgpu_buffer_rsrc_t rr = buf_rsrc(cf + (int64_t)m * sz * RS);
     const __amdgpu_buffer_rsrc_t rb = buf_rsrc(b + (int64_t)m * sz);
 #pragma unroll
@@ -2062,7 +2074,7 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
     }
   };
 
-  if (f_lo - 1 >= 0) {
+  if (f_lo - 1 >= ulo) {
     load_plane(f_lo - 1);
     put_plane(f_lo - 1);
   }
@@ -2072,13 +2084,13 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
   load_pts(f_lo);
   T win[4];
   int K = K0;
-  rtaps4<T>(K, gc.nz, cz, iz, wz);
+  ztaps(K);
   for (int f = f_lo; f <= f_hi; ++f) {
-    if (f + 1 < nz) put_plane(f + 1);
+    if (f + 1 < uhi) put_plane(f + 1);
     load_plane(f + 2);
     __syncthreads();  // ring planes f-1..f+1 staged; last plane's restriction reads of rt done
-    const int zm = f == 0 ? f + 1 : f - 1;
-    const int zp = f == nz - 1 ? f - 1 : f + 1;
+    const int zm = (f == 0 && !gf.zlo_ghost) ? f + 1 : f - 1;
+    const int zp = (f == nz - 1 && !gf.zhi_ghost) ? f - 1 : f + 1;
 #pragma unroll
     for (int e = 0; e < RPT; ++e) {
       if (e > 0 && !wave_in(e)) continue;
@@ -2137,7 +2149,7 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
           if (zx) zx[o] = T(0);
         }
         ++K;
-        if (K < K1) rtaps4<T>(K, gc.nz, cz, iz, wz);
+        if (K < K1) ztaps(K);
       }
     }
   }

@@ -593,6 +593,15 @@ class Solver final : public SolverBase {
   // (MAD_RR_G=1, measurement runs): bit-identical, but it issues 2.1x the VALU / LDS / SALU
   // instructions of resid_restrict3_k and runs 1.2-1.5x slower at 512^3 (DESIGN.md,
   // profiles/r02_rr_g_ab.md)
+  // the one-pass descent on rank slabs (MAD_RR_SLAB=0: residual + exchange + restriction
+  // there, A/B runs)
+  static bool rr_slab_env() {
+    static const bool v = [] {
+      const char* e = std::getenv("MAD_RR_SLAB");
+      return !(e && e[0] == '0');
+    }();
+    return v;
+  }
   static bool rr_g_env() {
     static const bool v = [] {
       const char* e = std::getenv("MAD_RR_G");
@@ -1214,9 +1223,21 @@ class Solver final : public SolverBase {
     }();
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
-    if (!on || c_->dim != 3 || c_->geom[l].distributed || c_->geom[l + 1].distributed ||
-        F.g.zlo_ghost || F.g.zhi_ghost || F.g.nx < 16 || F.g.ny < 16 || F.g.nz < 2)
+    // one GPU (or a replicated level), or a rank slab whose coarse level is a slab too (the
+    // taps past the slab residualise the fine ghost planes: x and b ghost planes made current
+    // first -- the b exchange stands in for the residual's)
+    const bool dist = c_->geom[l].distributed;
+    if (!on || c_->dim != 3 || dist != c_->geom[l + 1].distributed || F.g.nx < 16 || F.g.ny < 16 ||
+        F.g.nz < 2)
       return false;
+    if (dist && !rr_slab_env()) return false;
+    if (dist) {
+      halo(l, F.x, GHOST);
+      if (!F.brec && !F.b_halo_ok) {
+        halo(l, F.b, GHOST);
+        F.b_halo_ok = true;
+      }
+    }
     sync_brec(l);
     C.b_halo_ok = C.brec_ok = false;
     T* zx = zero_x ? C.x : nullptr;
@@ -1265,6 +1286,7 @@ class Solver final : public SolverBase {
       const char* e = std::getenv("MAD_RR_NT");  // tuning runs only: 512 or 1024 threads
       return e ? std::atoi(e) : 512;
     }();
+    const int ncz = (int)c_->geom[l + 1].n[2];  // global coarse nz (taps in global indices)
     auto run = [&](auto CXc, auto CYc, auto NTc) {
       constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = decltype(NTc)::value;
       const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
@@ -1277,11 +1299,11 @@ class Solver final : public SolverBase {
         if (F.brec)
           hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT, true>), grid, block, 0, c_->stream,
                              F.x, F.b, F.cf, F.g, F.rat, C.b, zx, C.g, C.cent[0], C.cent[1], C.cent[2],
-                             kc, ntx);
+                             kc, ntx, F.g.zoff, ncz);
         else
           hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT>), grid, block, 0, c_->stream, F.x,
                              F.b, F.cf, F.g, F.rat, C.b, zx, C.g, C.cent[0], C.cent[1], C.cent[2], kc,
-                             ntx);
+                             ntx, F.g.zoff, ncz);
       };
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
