@@ -623,12 +623,29 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
 // edge chunks then count themselves in sig[0] (bottom) / sig[1] (top), and the
 // communication stream, waiting on those counters, exchanges the halo while the rest
 // of the sweep runs -- one launch per sweep instead of boundary + interior launches.
-template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false>
+//
+// PROLONG (the V-cycle's first post-smoothing sweep, one rank): the sweep reads
+// x + P e_c instead of x -- the coarse-grid correction (MAD.hxx:422-435) folded into the
+// plane loads, with interp3_k's taps and arithmetic, so the result is bit-identical to
+// interp3_k followed by the sweep and level 0 skips interp3_k's x read-modify-write.  The
+// coarse planes the region's taps reach go through a 4-slot LDS ring after the fine ring,
+// one coarse plane loaded a step ahead.
+template <typename W>
+__device__ __forceinline__ void itaps2(int f, int nc, int cell, int* idx, W* w);  // (below)
+
+template <typename T>
+struct ProlongArgs {
+  const T* ec;  // coarse x (level l+1, dense; its sizes follow from the fine ones and the centring)
+  int cent;     // coarse centring flags (C.cent): x | y << 1 | z << 2
+};
+
+template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false,
+          bool PROLONG = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
                                                         int zbase, int zstride, int flip_last,
-                                                        uint32_t* __restrict__ sig) {
+                                                        uint32_t* __restrict__ sig, ProlongArgs<T> pa) {
   constexpr int NC = (KIND == KFULL) ? 4 : 2;
   using FG = FusedGeom<NC, TX, TY>;
   constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
@@ -707,6 +724,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   // a quarter of the issue-bound sweep's vector instructions.  -1 marks no element.
   uint32_t usrc[UPT];
   int udst[UPT];
+  uint32_t ucrd[PROLONG ? UPT : 1];  // PROLONG: the element's (mirrored) fine x | y << 16
 #pragma unroll
   for (int e = 0; e < UPT; ++e) {
     const int q = tid + e * NT;
@@ -718,6 +736,11 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     }
     usrc[e] = (uint32_t)(gj * sy + gi) * TS;
     udst[e] = (q < RX * RY) ? (int)((lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS) : -1;
+    // (clamped into the region too: only positions 2+ outside the domain change, whose values
+    // no stage point reads, and every tap then stays inside the coarse tile)
+    if constexpr (PROLONG)
+      ucrd[e] = (uint32_t)min(max(gi, max(rx0, 0)), min(rx0 + RX - 1, nx - 1)) |
+                ((uint32_t)min(max(gj, max(ry0, 0)), min(ry0 + RY - 1, ny - 1)) << 16);
   }
   int olds[OPT], oglb[OPT];
 #pragma unroll
@@ -812,11 +835,76 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     for (int e = 0; e < UPT; ++e) up[e] = buf_load<T, MAD_U_AUX>(rs, usrc[e], 0u);
 #endif
   };
+  // ---- PROLONG: coarse tile (region's taps), 4-slot ring after the fine ring
+  constexpr int CXW = RX / 2 + 3, CYW = RY / 2 + 3, CPL = CXW * CYW;
+  constexpr int CPT = PROLONG ? (CPL + NT - 1) / NT : 1;  // coarse tile elements per thread
+  T* cring = reinterpret_cast<T*>(fused_smem + (size_t)NP * PLANE * TS);
+  const int ccx0 = (rx0 >> 1) - 1, ccy0 = (ry0 >> 1) - 1;  // coarse tile origin (floor)
+  uint32_t csrc[CPT];
+  T creg[CPT];
+  int chi = -1;  // highest coarse plane put into the ring
+  // coarse sizes: a cell-centred axis halves, a vertex-centred one keeps both ends
+  const int pcx = pa.cent & 1, pcy = (pa.cent >> 1) & 1, pcz = (pa.cent >> 2) & 1;
+  const int cnx = pcx ? nx / 2 : (nx + 1) / 2, cny = pcy ? ny / 2 : (ny + 1) / 2;
+  const int cnz = pcz ? g.nz / 2 : (g.nz + 1) / 2;
+  const int64_t csz = (int64_t)cnx * cny;
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    csrc[q] = 0u;
+    creg[q] = T(0);
+    if constexpr (PROLONG) {
+      const int ce = min(tid + q * NT, CPL - 1);
+      const int lcy = ce / CXW, lcx = ce - (ce / CXW) * CXW;
+      csrc[q] = (uint32_t)(min(max(ccy0 + lcy, 0), cny - 1) * cnx + min(max(ccx0 + lcx, 0), cnx - 1)) * TS;
+    }
+  }
+  auto cload = [&](int K) {
+    const __amdgpu_buffer_rsrc_t rc = buf_rsrc(pa.ec + (int64_t)min(max(K, 0), cnz - 1) * csz);
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) creg[q] = buf_load<T>(rc, csrc[q], 0u);
+  };
+  auto cput = [&](int K) {
+#pragma unroll
+    for (int q = 0; q < CPT; ++q)
+      if (tid + q * NT < CPL) cring[(K & 3) * CPL + tid + q * NT] = creg[q];
+  };
+  // the coarse planes fine plane m's taps reach: up to (m >> 1) + 1 (clamped)
+  auto ctop = [&](int m) { return min(max(m + g.zoff, 0) / 2 + 1, cnz - 1); };
+  // x + P e_c at element e of fine plane m (interp3_k's taps and fma order)
+  auto prolong = [&](int e, int m, T xc) -> T {
+#pragma clang fp contract(off)
+    const int gi = (int)(ucrd[e] & 0xffffu), gj = (int)(ucrd[e] >> 16);
+    int ix[2], iy[2], iz[2];
+    T wx[2], wy[2], wz[2];
+    itaps2<T>(gi, cnx, pcx, ix, wx);
+    itaps2<T>(gj, cny, pcy, iy, wy);
+    itaps2<T>(m + g.zoff, cnz, pcz, iz, wz);
+    T v = T(0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const T* pl = cring + (iz[c] & 3) * CPL - ccx0;
+      T vz = T(0);
+#pragma unroll
+      for (int bq = 0; bq < 2; ++bq) {
+        const T* row = pl + (iy[bq] - ccy0) * CXW;
+        vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
+      }
+      v = fma(wz[c], vz, v);
+    }
+    return xc + v;
+  };
   auto put_plane = [&](int m) {
     unsigned char* P = lbytes + slot(m) * (PLANE * TS);
 #pragma unroll
-    for (int e = 0; e < UPT; ++e)
-      if (e < UPT - 1 || udst[e] >= 0) *reinterpret_cast<T*>(P + udst[e]) = up[e];
+    for (int e = 0; e < UPT; ++e) {
+      if (e < UPT - 1 || udst[e] >= 0) {
+        T val = up[e];
+        if constexpr (PROLONG) val = prolong(e, m, val);
+        *reinterpret_cast<T*>(P + udst[e]) = val;
+      }
+      // one element at a time: the sweep has few registers to spare
+      if constexpr (PROLONG) __builtin_amdgcn_sched_barrier(0);
+    }
   };
   // stage c data of step k (plane m = k - c, parity PM)
   // unconditional (the plane index clamped into the loadable range): a conditional
@@ -909,6 +997,17 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   };
 
   // prologue: planes kbeg-1, kbeg into LDS; plane kbeg+1 and step kbeg's stage data
+  if constexpr (PROLONG) {
+    // coarse planes of fine planes kbeg-1 .. kbeg+1 (the puts of the prologue and step kbeg)
+    const int c0 = max(max(kbeg - 1 + g.zoff, 0) / 2 - 1, 0), c1 = ctop(kbeg + 1);
+    for (int K = c0; K <= c1; ++K) {
+      cload(K);
+      cput(K);
+    }
+    chi = c1;
+    if (chi + 1 <= ctop(kbeg + 2)) cload(chi + 1);
+    __syncthreads();
+  }
   for (int m = kbeg - 1; m <= kbeg; ++m)
     if (plane_ok(m)) {
       load_plane(m);
@@ -927,6 +1026,14 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
         // (stage, parity, flag) test out of the loop as a 64-bit lane mask and spills
         asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(omask));
         if (plane_ok(k + 1)) put_plane(k + 1);
+        if constexpr (PROLONG) {
+          // the coarse plane fine plane k+2 (put next step) needs, and the one after it
+          if (chi < ctop(k + 2)) {
+            ++chi;
+            cput(chi);
+          }
+          if (chi < ctop(k + 3)) cload(chi + 1);
+        }
         load_plane(k + 2);
         __syncthreads();
 #pragma unroll

@@ -696,7 +696,7 @@ class Solver final : public SolverBase {
   }
 
   template <int KD, int TX, int TY, int NT>
-  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part) {
+  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part, bool prolong = false) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
     const int nz = L.g.nz;
@@ -732,27 +732,47 @@ class Solver final : public SolverBase {
     constexpr int NC = (KD == KFULL) ? 4 : 2;
     using FG = FusedGeom<NC, TX, TY>;
     constexpr size_t lds = sizeof(T) * FG::NP * FG::PLANE;
+    // PROLONG: + the 4-slot coarse ring (gs_fused3_k)
+    constexpr size_t lds_p = lds + sizeof(T) * 4 * (FG::RX / 2 + 3) * (FG::RY / 2 + 3);
     REQUIRE(lds <= 160 * 1024, MAD_ERR_UNSUPPORTED,
             "fused GS tile needs " + std::to_string(lds) + " B of LDS (> 160 KiB)");
     // fp64 doubles the register footprint: 2 waves per SIMD (one 512-thread block per CU,
     // which is all its LDS allows anyway)
     constexpr int MW = sizeof(T) == 8 ? 2 : 4;
-    auto run = [&](auto kern) {
+    ProlongArgs<T> pa{};
+    auto run = [&](auto kern, size_t bytes) {
       static bool attr = false;
       if (!attr) {
         HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
+                                      (int)bytes));
         attr = true;
       }
-      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), bytes, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
+                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, pa);
     };
+    if (prolong) {
+      // the first post-smoothing sweep of a V-cycle with x + P e_c folded into its loads
+      // (prolong_fold_ok: one rank, whole slab, the default full-tensor tile)
+      REQUIRE(part == 0 && flip == 0 && !L.brec, MAD_ERR_STATE, "prolongation fold on a plain sweep only");
+      if constexpr (KD == KFULL && ((sizeof(T) == 4 && TX == 64 && TY == 32 && NT == 1024) ||
+                                    (sizeof(T) == 8 && TX == 64 && TY == 16 && NT == 512))) {
+        const LevelData<T>& C = *(&L + 1);
+        REQUIRE(C.g.nx == (C.cent[0] ? L.g.nx / 2 : (L.g.nx + 1) / 2) &&
+                    C.g.ny == (C.cent[1] ? L.g.ny / 2 : (L.g.ny + 1) / 2) &&
+                    C.g.nz == (C.cent[2] ? L.g.nz / 2 : (L.g.nz + 1) / 2) && C.g.sy == C.g.nx,
+                MAD_ERR_STATE, "prolongation fold: unexpected coarse geometry");
+        pa = ProlongArgs<T>{C.x, (C.cent[0] ? 1 : 0) | (C.cent[1] ? 2 : 0) | (C.cent[2] ? 4 : 0)};
+        run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>, lds_p);
+        return;
+      }
+      throw MadError(MAD_ERR_STATE, "prolongation fold: no kernel for this tile");
+    }
     if (L.brec)
-      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>, lds);
     else if (KD == KFULL && fc.lead == 3)
-      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>);
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>, lds);
     else
-      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>, lds);
   }
 
 
@@ -779,7 +799,7 @@ class Solver final : public SolverBase {
     *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
   }
 
-  void launch_fused_part(LevelData<T>& L, int part) {
+  void launch_fused_part(LevelData<T>& L, int part, bool prolong = false) {
     const FusedCfg& fc = fused_cfg();
     if (fusedg_on(L)) {
       if constexpr (sizeof(T) == 8) {
@@ -794,13 +814,13 @@ class Solver final : public SolverBase {
       }
     } else if (c_->kind == KFULL) {
       if (fc.tile == 1)
-        launch_fused<KFULL, 64, 32, 1024>(L, fc, part);
+        launch_fused<KFULL, 64, 32, 1024>(L, fc, part, prolong);
       else if (fc.tile == 2)
-        launch_fused<KFULL, 128, 16, 1024>(L, fc, part);
+        launch_fused<KFULL, 128, 16, 1024>(L, fc, part, prolong);
       else if (fc.tile == 3)
-        launch_fused<KFULL, 128, 8, 512>(L, fc, part);
+        launch_fused<KFULL, 128, 8, 512>(L, fc, part, prolong);
       else
-        launch_fused<KFULL, 64, 16, 512>(L, fc, part);
+        launch_fused<KFULL, 64, 16, 512>(L, fc, part, prolong);
     } else if (c_->kind == KDIAG) {
       launch_fused<KDIAG, 64, 16, 1024>(L, fc, part);
     } else {
@@ -927,7 +947,6 @@ class Solver final : public SolverBase {
       L.b_halo_ok = true;
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
-    const bool dist = c_->comm.active() && c_->geom[l].distributed;
     const bool overlap = sweep_overlap(l);
     int tiles = 0, nchunks = 0;
     if (overlap) fused_shape(L, &tiles, &nchunks);
@@ -950,7 +969,10 @@ class Solver final : public SolverBase {
       // MAD_SPLIT_PROXY=1 (measurement only): launch a single-GPU slab as a rank slab's
       // boundary + interior parts, without the exchange (tools/bench_slab.py)
       static const bool proxy = std::getenv("MAD_SPLIT_PROXY") != nullptr;
-      if (proxy && c_->d.gs_kernel != 2 && L.g.nz >= 3 * boundary_planes()) {
+      if (prolong_l_ == l) {  // the V-cycle's correction, folded into this sweep's loads
+        prolong_l_ = -1;
+        launch_fused_part(L, 0, true);
+      } else if (proxy && c_->d.gs_kernel != 2 && L.g.nz >= 3 * boundary_planes()) {
         launch_fused_part(L, 1);
         launch_fused_part(L, 2);
       } else {
@@ -1407,7 +1429,10 @@ class Solver final : public SolverBase {
       fill(l + 1, MAD_X, 0.0);  // MAD.hxx:415-416
     }
     vcycle_rec(l + 1);        // MAD.hxx:418-420
-    interpolate_up(l, true);  // MAD.hxx:422-435
+    if (prolong_fold_ok(l))   // MAD.hxx:422-435: x += P x_c inside the first post-sweep
+      prolong_l_ = l;
+    else
+      interpolate_up(l, true);
     if (c_->d.verbose) verbose_line(l, 0, "initial");
     if (c_->d.verbose) {
       for (unsigned n = 0; n < nu; ++n) {
@@ -1619,6 +1644,28 @@ class Solver final : public SolverBase {
   }
 
   void vcycle() override { vcycle_fast(); }
+
+  // The V-cycle's prolongation + add folded into level l's first post-smoothing sweep
+  // (gs_fused3_k<..., PROLONG>): one rank, full tensor, the fused sweep in its default tile on
+  // a whole slab (gs_kernel 0 / 3), no verbose trace (it prints the norm of the corrected x
+  // before smoothing).  Bit-identical to interp3_k + the sweep (test_prolongation_fold_is_bitwise).
+  // Opt-in (MAD_PROLONG_FOLD=1, measurement runs): the sweep kernel is at the SGPR limit
+  // already, the fold's uniform state spills (23 SGPR / 14 VGPR), and the folded level-0 +
+  // level-1 sweeps took 2.01 ms per cycle against 1.47 + 0.30 ms for the sweeps + interp3_k
+  // (profiles/r02_prolong_fold_ab.md).
+  int prolong_l_ = -1;
+  bool prolong_fold_ok(int l) const {
+    static const bool env = [] {
+      const char* e = std::getenv("MAD_PROLONG_FOLD");
+      return e && e[0] == '1';
+    }();
+    const FusedCfg& fc = fused_cfg();
+    const int def_tile = sizeof(T) == 4 ? 1 : 0;
+    return env && c_->dim == 3 && !c_->comm.active() && !c_->d.verbose && c_->kind == KFULL &&
+           c_->d.smoother == MAD_GAUSS_SEIDEL && (c_->d.gs_kernel == 0 || c_->d.gs_kernel == 3) &&
+           c_->d.iterations_per_grid >= 1 && use_fused(l) && !fusedg_on(lv_[l]) && !lv_[l].brec &&
+           fc.tile == def_tile;
+  }
   void fmg() override { fmg_rec(0); }
 
   void verbose_line(int l, int it, const char* what) {

@@ -311,3 +311,39 @@ def test_vcycle_starts_coarse_levels_from_zero(shape, prec):
         out.append(s.download(0, M.capi.X))
     s.close()
     assert np.array_equal(out[0], out[1])
+
+
+def test_prolongation_fold_is_bitwise(tmp_path):
+    """The V-cycle's prolongation + add folded into the first post-smoothing fused sweep
+    (gs_fused3_k<..., PROLONG>: the sweep loads x + P e_c through a coarse LDS ring; opt-in,
+    MAD_PROLONG_FOLD=1, measured slower) equals interp3_k followed by the sweep
+    (the default) bit for bit, both in child processes: two V-cycles on a level-0 grid large
+    enough for the fused sweep, odd / even axes, fp32 and fp64."""
+    import os
+    import subprocess
+    import sys
+    import multigridanisotropicdiffusion_amd as M
+    import synth
+    here = os.path.dirname(os.path.abspath(__file__))
+    shape = (64, 258, 257)  # 4.2 M voxels: level 0 sweeps fused; vertex-centred x (odd)
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "import multigridanisotropicdiffusion_amd as M, synth\n"
+            "shape = %r\n"
+            "for p in ('FP32', 'FP64'):\n"
+            "    s = M.Solver(shape, (1.0, 0.9, 1.2), time_step=0.5, precision=getattr(M, p))\n"
+            "    s.set_tensor(synth.random_spd(shape, seed=21))\n"
+            "    s.setup()\n"
+            "    s.upload(0, M.capi.X, synth.image(shape, seed=22))\n"
+            "    s.upload(0, M.capi.B, synth.image(shape, seed=23))\n"
+            "    s.vcycle(); s.vcycle()\n"
+            "    np.save(%r + '/x_%%s.npy' %% p, s.download(0, M.capi.X))\n"
+            "    s.close()\n") % (os.path.dirname(here), here, shape, str(tmp_path))
+    outs = {}
+    for fold in ("0", "1"):
+        env = dict(os.environ, MAD_PROLONG_FOLD=fold)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs[fold] = {p: np.load(tmp_path / f"x_{p}.npy") for p in ("FP32", "FP64")}
+    for p in ("FP32", "FP64"):
+        assert np.array_equal(outs["0"][p], outs["1"][p]), (p, np.abs(outs["0"][p] - outs["1"][p]).max())
