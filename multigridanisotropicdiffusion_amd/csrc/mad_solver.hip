@@ -871,8 +871,9 @@ class Solver final : public SolverBase {
       }
       const bool brec = lv_[l].brec;
       const int lead = (!brec && kind == KFULL && fc.lead == 3) ? 3 : 2;
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d%s>", tn, kind, tx, ty,
-                    nt, sizeof(T) == 8 ? 2 : 4, lead, brec ? ", true" : "");
+      // every template argument, as rocprofv3 prints the instantiation (BREC, PROLONG last)
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d, %s, false>", tn, kind, tx,
+                    ty, nt, sizeof(T) == 8 ? 2 : 4, lead, brec ? "true" : "false");
       // rank slabs: which sweep form fused_sweep takes
       const LevelData<T>& L = lv_[l];
       if (sweep_overlap(l)) {
