@@ -42,7 +42,11 @@ typedef enum mad_status {
   MAD_ERR_SINGULAR = 5,    /* coarsest operator singular */
   MAD_ERR_UNSUPPORTED = 6, /* valid request this build does not implement */
   MAD_ERR_NOMEM = 7,
-  MAD_ERR_NUMERIC = 8      /* NaN/Inf residual norm or diffusion tensor */
+  MAD_ERR_NUMERIC = 8,     /* NaN/Inf residual norm or diffusion tensor */
+  MAD_ERR_NOT_CONVERGED = 9 /* warning, not a failure: the stall guard ended a time step above
+                               Tolerance (the storage precision's floor, e.g. MAD_FP32 asked for
+                               1e-10).  The output image and the stats are written; the reference
+                               would have run on to MaxCycles (MAD.hxx:207-246). */
 } mad_status;
 
 /* MAD.h:123 enum CycleType { VCYCLE, FMG, SMOOTHER } -- same values */
@@ -65,8 +69,15 @@ typedef enum mad_dtype {
 
 /* MAD_FP32_REFINE: fp32 hierarchy (storage + arithmetic) inside a mixed-precision defect
    correction -- level 0's iterate, rhs and residual in fp64 with the fp64 operator, one fp32
-   cycle per correction -- so a solve reaches the reference's fp64 tolerances (1e-10) */
-typedef enum mad_precision { MAD_FP32 = 0, MAD_FP64 = 1, MAD_FP32_REFINE = 2 } mad_precision;
+   cycle per correction -- so a solve reaches the reference's fp64 tolerances (1e-10).
+   MAD_PRECISION_AUTO (the mad_desc_init default) is resolved by mad_create from the tolerance:
+   MAD_FP32_REFINE when tolerance < 1e-6 (below what fp32 storage resolves; e.g. the reference
+   tests' 1e-10, test/itk2DDiffusionTest_GS.cxx:97, test/itkVEDTest_GS.cxx:85), MAD_FP32
+   otherwise; mad_get_desc then reports the resolved value */
+typedef enum mad_precision {
+  MAD_FP32 = 0, MAD_FP64 = 1, MAD_FP32_REFINE = 2, MAD_PRECISION_AUTO = 3
+} mad_precision;
+#define MAD_FP32_TOLERANCE_FLOOR 1e-6
 
 typedef enum mad_tensor_kind {
   MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */
@@ -95,10 +106,12 @@ typedef struct mad_desc {
   double tolerance;              /* SetTolerance,          default 1e-6 */
   double omega;                  /* WJ weight (MultigridWeightedJacobiSmoother ctor), default 2/3 */
   int32_t verbose;               /* SetVerbose,            default 0 */
-  int32_t precision;             /* MAD_FP32 (default), MAD_FP64 storage + arithmetic, or
-                                    MAD_FP32_REFINE (fp32 cycles, fp64 defect correction) */
-  int32_t stall_guard;           /* 1: end a time step once relres stops improving (the fp32
-                                    floor); default 1 for FP32 / FP32_REFINE, 0 for FP64 */
+  int32_t precision;             /* MAD_PRECISION_AUTO (default), MAD_FP32, MAD_FP64 storage +
+                                    arithmetic, or MAD_FP32_REFINE (fp32 cycles, fp64 defect
+                                    correction) */
+  int32_t stall_guard;           /* 1: end a time step once relres stops improving (a precision
+                                    floor) -- mad_run then returns MAD_ERR_NOT_CONVERGED; default 1
+                                    (the FP64 path never stalls above 1e-13) */
   int32_t device;                /* HIP device ordinal, -1 = current device */
   int32_t tensor_kind;           /* mad_tensor_kind, default AUTO */
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
@@ -160,6 +173,14 @@ int mad_run_device(mad_ctx *ctx, const void *dev_in, int32_t in_dtype, void *dev
                    int32_t out_dtype, mad_stats *stats);
 /* per-time-step history of the last run */
 int mad_get_step_stats(const mad_ctx *ctx, uint32_t step, uint32_t *cycles, double *relres);
+/* Convergence history of the last run, one entry per cycle (V-cycle / FMG cycle / smoother
+ * sweep): the time step it belongs to, the relative residual ||b - A x|| / ||b|| after it and
+ * the seconds since the run started (host wall clock, the norm is read back every cycle).
+ * The reference writes the same pairs to benchmark.txt under -DBENCHMARK
+ * (MAD.hxx:147-151, 222-227).  Copies min(cap, total) entries (any pointer may be NULL);
+ * *count = total entries of the run. */
+int mad_get_cycle_trace(const mad_ctx *ctx, uint32_t cap, uint32_t *step, double *relres,
+                        double *seconds, uint32_t *count);
 
 /* ---------------------------------------------------------------- hierarchy */
 int mad_num_levels(const mad_ctx *ctx);               /* GH::GetMaxDepth() + 1 */

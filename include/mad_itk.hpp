@@ -16,6 +16,7 @@
 
 #include <array>
 #include <cstdint>
+#include <iostream>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -111,6 +112,17 @@ inline void check(int rc, const mad_ctx* c = nullptr) {
   if (rc != MAD_OK) throw Error(rc, std::string("mad: ") + mad_last_error(c));
 }
 
+// MAD_ERR_NOT_CONVERGED is a warning (the output is written), as an ITK filter would report it
+// with itkWarningMacro instead of an exception; returns false then
+inline bool check_run(int rc, const char* what, const char* msg) {
+  if (rc == MAD_ERR_NOT_CONVERGED) {
+    std::cerr << "WARNING: " << what << ": " << msg << std::endl;
+    return false;
+  }
+  if (rc != MAD_OK) throw Error(rc, std::string(what) + ": " + msg);
+  return true;
+}
+
 template <class TInputImage, class TOutputImage,
           class TSmootherType = MultigridGaussSeidelSmoother<TInputImage::ImageDimension>>
 class MultigridAnisotropicDiffusionImageFilter {
@@ -172,10 +184,12 @@ class MultigridAnisotropicDiffusionImageFilter {
     output_->Allocate();
     output_->SetSpacing(input_->GetSpacing());
     output_->SetOrigin(input_->GetOrigin());  // .hxx:286
-    check(mad_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
-                  output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id, &stats_),
-          ctx_);
+    const int rc = mad_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
+                           output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id, &stats_);
+    converged_ = check_run(rc, "mad", mad_last_error(ctx_));
   }
+  // false when the stall guard ended a time step above the tolerance (MAD_ERR_NOT_CONVERGED)
+  bool GetConverged() const { return converged_; }
 
  protected:
   MultigridAnisotropicDiffusionImageFilter() { check(mad_desc_init(&desc_)); }
@@ -184,6 +198,7 @@ class MultigridAnisotropicDiffusionImageFilter {
   mad_desc desc_{};
   mad_ctx* ctx_ = nullptr;
   mad_stats stats_{};
+  bool converged_ = true;
   const TInputImage* input_ = nullptr;
   std::vector<double> tensor_;
   typename TOutputImage::Pointer output_;
@@ -251,11 +266,12 @@ class VEDMultigridImageFilter {
     output_->Allocate();
     output_->SetSpacing(input_->GetSpacing());
     output_->SetOrigin(input_->GetOrigin());
-    if (int rc = mad_ved_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
-                             output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id,
-                             &stats_))
-      throw Error(rc, std::string("mad_ved: ") + mad_ved_last_error(ctx_));
+    const int rc = mad_ved_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
+                               output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id,
+                               &stats_);
+    converged_ = check_run(rc, "mad_ved", mad_ved_last_error(ctx_));
   }
+  bool GetConverged() const { return converged_; }
 
  protected:
   VEDMultigridImageFilter() { check(mad_ved_desc_init(&desc_)); }
@@ -264,6 +280,7 @@ class VEDMultigridImageFilter {
   mad_ved_desc desc_{};
   mad_ved_ctx* ctx_ = nullptr;
   mad_ved_stats stats_{};
+  bool converged_ = true;
   const TInputImage* input_ = nullptr;
   typename TOutputImage::Pointer output_;
 };

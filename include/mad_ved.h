@@ -54,7 +54,9 @@ typedef struct mad_ved_desc {
   int32_t verbose;                 /* 0 */
   /* additions (no reference counterpart) */
   int32_t smoother;                /* mad_smoother, default MAD_GAUSS_SEIDEL (VED.h:44) */
-  int32_t precision;               /* MAD_FP32 (default) / MAD_FP64: Hessian and solver storage */
+  int32_t precision;               /* MAD_PRECISION_AUTO (default) / MAD_FP32 / MAD_FP32_REFINE: fp32
+                                      Hessian, the diffusion solve as mad_create resolves it (AUTO:
+                                      FP32_REFINE below tolerance 1e-6); MAD_FP64: fp64 throughout */
   int32_t device;                  /* HIP device, -1 = current */
   int32_t nranks;                  /* z-slab ranks of the diffusion step (1 = single GPU) */
   int32_t rank;

@@ -6,8 +6,8 @@ ABI in include/mad.h).  This package is the host-side mirror of the reference's
 operator surface; it never falls back to a CPU implementation.
 """
 from . import _capi as capi
-from ._capi import (FMG, FP32, FP32_REFINE, FP64, GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, SMOOTHER, VCYCLE,
-                    WEIGHTED_JACOBI, MadError)
+from ._capi import (FMG, FP32, FP32_REFINE, FP64, GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, PRECISION_AUTO,
+                    SMOOTHER, VCYCLE, WEIGHTED_JACOBI, MadError, NotConvergedWarning)
 from .filters import (Image, MultigridAnisotropicDiffusionImageFilter,
                       MultigridGaussSeidelLexSmoother, MultigridGaussSeidelSmoother,
                       MultigridWeightedJacobiSmoother, TensorImage)
@@ -20,5 +20,5 @@ __all__ = [
     "MultigridAnisotropicDiffusionImageFilter", "MultigridGaussSeidelSmoother",
     "MultigridGaussSeidelLexSmoother", "MultigridWeightedJacobiSmoother", "MadError",
     "VCYCLE", "FMG", "SMOOTHER", "GAUSS_SEIDEL", "GAUSS_SEIDEL_LEX", "WEIGHTED_JACOBI",
-    "FP32", "FP32_REFINE", "FP64", "VED", "VEDMultigridImageFilter", "mhd",
+    "FP32", "FP32_REFINE", "FP64", "PRECISION_AUTO", "NotConvergedWarning", "VED", "VEDMultigridImageFilter", "mhd",
 ]

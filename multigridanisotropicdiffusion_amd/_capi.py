@@ -14,15 +14,15 @@ ABI_VERSION = 1
 
 # mad_status
 OK, ERR_INVALID, ERR_STATE, ERR_DEVICE, ERR_COMM, ERR_SINGULAR, ERR_UNSUPPORTED, ERR_NOMEM, \
-    ERR_NUMERIC = range(9)
+    ERR_NUMERIC, ERR_NOT_CONVERGED = range(10)
 # mad_cycle (itkMultigridAnisotropicDiffusionImageFilter.h:123)
 VCYCLE, FMG, SMOOTHER = 0, 1, 2
 # mad_smoother
 GAUSS_SEIDEL, GAUSS_SEIDEL_LEX, WEIGHTED_JACOBI = 0, 1, 2
 # mad_dtype
 U8, I8, U16, I16, U32, I32, F32, F64 = range(8)
-# mad_precision
-FP32, FP64, FP32_REFINE = 0, 1, 2
+# mad_precision (PRECISION_AUTO, the default: FP32_REFINE below tolerance 1e-6, else FP32)
+FP32, FP64, FP32_REFINE, PRECISION_AUTO = 0, 1, 2, 3
 # mad_ved_hessian_kind
 VED_HESSIAN_RECURSIVE, VED_HESSIAN_FIR = 0, 1
 # mad_tensor_kind
@@ -33,7 +33,7 @@ X, B, R = 0, 1, 2
 EXPORTS = (
     "mad_desc_init", "mad_max_depth", "mad_create", "mad_destroy", "mad_last_error",
     "mad_get_desc", "mad_set_tensor", "mad_set_tensor_device", "mad_setup", "mad_run",
-    "mad_run_device", "mad_get_step_stats", "mad_num_levels", "mad_plan_level",
+    "mad_run_device", "mad_get_step_stats", "mad_get_cycle_trace", "mad_num_levels", "mad_plan_level",
     "mad_level_info", "mad_upload",
     "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
     "mad_residual_restrict",
@@ -181,6 +181,7 @@ def load():
         "mad_run": ([vp, vp, i32, vp, i32, ctypes.POINTER(MadStats)], i32),
         "mad_run_device": ([vp, vp, i32, vp, i32, ctypes.POINTER(MadStats)], i32),
         "mad_get_step_stats": ([vp, u32, u32p, dp], i32),
+        "mad_get_cycle_trace": ([vp, u32, u32p, dp, dp, u32p], i32),
         "mad_num_levels": ([vp], i32),
         "mad_plan_level": ([ctypes.POINTER(MadDesc), i32, i64p, dp, i32p, i64p, i64p, i32p], i32),
         "mad_level_info": ([vp, i32, i64p, dp, i32p], i32),
@@ -231,10 +232,20 @@ def load():
     return L
 
 
-def check(rc, ctx=None):
+class NotConvergedWarning(RuntimeWarning):
+    """MAD_ERR_NOT_CONVERGED: the stall guard ended a time step above Tolerance (the output
+    is still written); the ITK filter would report it as a warning."""
+
+
+def check(rc, ctx=None, warn_not_converged=False, last_error=None):
     if rc != OK:
-        msg = load().mad_last_error(ctx)
-        raise MadError(rc, msg.decode() if msg else "")
+        msg = (last_error or load().mad_last_error)(ctx)
+        msg = msg.decode() if msg else ""
+        if rc == ERR_NOT_CONVERGED and warn_not_converged:
+            import warnings
+            warnings.warn(msg, NotConvergedWarning, stacklevel=3)
+            return rc
+        raise MadError(rc, msg)
     return rc
 
 

@@ -206,6 +206,13 @@ struct mad_ctx {
   std::unique_ptr<SolverBase> solver;
   std::vector<uint32_t> step_cycles;
   std::vector<double> step_relres;
+  // per-cycle convergence history of the last run (mad_get_cycle_trace; the reference's
+  // BENCHMARK trace, MAD.hxx:147-151, 222-227)
+  struct TracePoint {
+    uint32_t step;
+    double relres, seconds;
+  };
+  std::vector<TracePoint> trace;
   double setup_ms = 0.0;
   Comm comm;
   ~mad_ctx();
@@ -1714,6 +1721,11 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipEventRecord(e0, c_->stream));
     c_->step_cycles.clear();
     c_->step_relres.clear();
+    c_->trace.clear();
+    const auto t_run = std::chrono::steady_clock::now();
+    auto trace = [&](unsigned step, double rr) {
+      c_->trace.push_back({step, rr, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count()});
+    };
     bool stalled_any = false;
     unsigned total = 0;
     double relres = 0.0;
@@ -1753,6 +1765,7 @@ class Solver final : public SolverBase {
         if (d.verbose && d.cycle == MAD_SMOOTHER && c_->comm.rank() == 0)
           std::printf("Smoother iteration n. %u: relative residual = %g\n", it + 1, relres);
         ++it;
+        trace(step, relres);
         hist.push_back(relres);
         // fp32 floor guard: best relres not improved by 1% within `window` cycles
         if (d.stall_guard && hist.size() > window && relres < 1e-3) {
@@ -1833,6 +1846,11 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipEventRecord(e0, c_->stream));
     c_->step_cycles.clear();
     c_->step_relres.clear();
+    c_->trace.clear();
+    const auto t_run = std::chrono::steady_clock::now();
+    auto trace = [&](unsigned step, double rr) {
+      c_->trace.push_back({step, rr, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count()});
+    };
     bool stalled_any = false;
     unsigned total = 0;
     double relres = 0.0;
@@ -1877,6 +1895,7 @@ class Solver final : public SolverBase {
         if (d.verbose && d.cycle == MAD_SMOOTHER && c_->comm.rank() == 0)
           std::printf("Smoother iteration n. %u: relative residual = %g\n", it + 1, relres);
         ++it;
+        trace(step, relres);
         hist.push_back(relres);
         // fallback only: the fp64 residual keeps falling where plain fp32 stalls
         if (d.stall_guard && hist.size() > window && relres < 1e-3) {
@@ -2523,7 +2542,7 @@ int mad_desc_init(mad_desc* d) {
   d->tolerance = 1e-6;                 // MAD.hxx:43
   d->omega = 2.0 / 3.0;                // itkMultigridWeightedJacobiSmoother.hxx:189
   d->verbose = 0;                      // MAD.hxx:45
-  d->precision = MAD_FP32;
+  d->precision = MAD_PRECISION_AUTO;  // resolved by mad_create from the tolerance
   d->stall_guard = 1;
   d->device = -1;
   d->tensor_kind = MAD_TENSOR_AUTO;
@@ -2560,14 +2579,19 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
     REQUIRE(d->cycle >= MAD_VCYCLE && d->cycle <= MAD_SMOOTHER, MAD_ERR_INVALID, "bad cycle");
     REQUIRE(d->smoother >= MAD_GAUSS_SEIDEL && d->smoother <= MAD_WEIGHTED_JACOBI,
             MAD_ERR_INVALID, "bad smoother");
-    REQUIRE(d->precision == MAD_FP32 || d->precision == MAD_FP64 || d->precision == MAD_FP32_REFINE,
-            MAD_ERR_INVALID,
-            "bad precision");
+    REQUIRE(d->precision == MAD_FP32 || d->precision == MAD_FP64 || d->precision == MAD_FP32_REFINE ||
+                d->precision == MAD_PRECISION_AUTO,
+            MAD_ERR_INVALID, "bad precision");
     REQUIRE(d->nranks >= 1 && d->rank >= 0 && d->rank < d->nranks, MAD_ERR_INVALID,
             "bad rank / nranks");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");
     c->d = *d;
+    // the default precision: fp32 storage resolves relres down to ~2e-7..8e-7
+    // (profiles/r02_refine_cycles.md); a tolerance below MAD_FP32_TOLERANCE_FLOOR (the
+    // reference tests ask for 1e-10) needs the fp64 defect correction to be reached
+    if (c->d.precision == MAD_PRECISION_AUTO)
+      c->d.precision = d->tolerance < MAD_FP32_TOLERANCE_FLOOR ? MAD_FP32_REFINE : MAD_FP32;
     if (c->d.dim == 2) c->d.size[2] = 1;
     c->dim = d->dim;
     int dev = d->device;
@@ -2723,20 +2747,51 @@ static int run_impl(mad_ctx* c, const void* in, int32_t in_dtype, void* out, int
   });
 }
 
+// MAD_ERR_NOT_CONVERGED when the stall guard ended a step above Tolerance (the output and
+// the stats are written): a port that asks fp32 storage for 1e-10 learns it from the status,
+// not only from stats.stalled
+static int run_status(mad_ctx* c, int rc, const mad_stats& st) {
+  if (rc != MAD_OK || !st.stalled) return rc;
+  char buf[256];
+  std::snprintf(buf, sizeof buf,
+                "tolerance %g not reached: the stall guard ended a time step at relres %g (the %s "
+                "floor); MAD_FP32_REFINE or MAD_FP64 reach the reference tolerances",
+                c->d.tolerance, st.last_relres, c->d.precision == MAD_FP64 ? "fp64" : "fp32");
+  c->err = buf;
+  return MAD_ERR_NOT_CONVERGED;
+}
+
 int mad_run(mad_ctx* c, const void* in, int32_t in_dtype, void* out, int32_t out_dtype,
             mad_stats* st) {
-  return run_impl(c, in, in_dtype, out, out_dtype, st, false);
+  mad_stats local{};
+  mad_stats* s = st ? st : &local;
+  return run_status(c, run_impl(c, in, in_dtype, out, out_dtype, s, false), *s);
 }
 
 int mad_run_device(mad_ctx* c, const void* in, int32_t in_dtype, void* out, int32_t out_dtype,
                    mad_stats* st) {
-  return run_impl(c, in, in_dtype, out, out_dtype, st, true);
+  mad_stats local{};
+  mad_stats* s = st ? st : &local;
+  return run_status(c, run_impl(c, in, in_dtype, out, out_dtype, s, true), *s);
 }
 
 int mad_get_step_stats(const mad_ctx* c, uint32_t step, uint32_t* cycles, double* relres) {
   if (!c || step >= c->step_cycles.size()) return MAD_ERR_INVALID;
   if (cycles) *cycles = c->step_cycles[step];
   if (relres) *relres = c->step_relres[step];
+  return MAD_OK;
+}
+
+int mad_get_cycle_trace(const mad_ctx* c, uint32_t cap, uint32_t* step, double* relres,
+                        double* seconds, uint32_t* count) {
+  if (!c) return MAD_ERR_INVALID;
+  const size_t n = c->trace.size();
+  for (size_t q = 0; q < n && q < cap; ++q) {
+    if (step) step[q] = c->trace[q].step;
+    if (relres) relres[q] = c->trace[q].relres;
+    if (seconds) seconds[q] = c->trace[q].seconds;
+  }
+  if (count) *count = (uint32_t)n;
   return MAD_OK;
 }
 

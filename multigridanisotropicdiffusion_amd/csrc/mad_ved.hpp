@@ -524,7 +524,7 @@ int mad_ved_desc_init(mad_ved_desc* d) {
   const double sc[5] = {0.300, 0.482, 0.775, 1.245, 2.000};
   for (int q = 0; q < 5; ++q) d->scales[q] = sc[q];
   d->smoother = MAD_GAUSS_SEIDEL;
-  d->precision = MAD_FP32;
+  d->precision = MAD_PRECISION_AUTO;  // Hessian in fp32; the diffusion solve as mad_create resolves it
   d->device = -1;
   d->nranks = 1;
   d->rank = 0;
@@ -584,16 +584,28 @@ void mad_ved_destroy(mad_ved_ctx* v) { delete v; }
 
 const char* mad_ved_last_error(const mad_ved_ctx* v) { return v ? v->err.c_str() : g_last_error.c_str(); }
 
+// as mad_run: MAD_ERR_NOT_CONVERGED (output written) when a diffusion step stalled above Tolerance
+static int ved_run_status(mad_ved_ctx* v, int rc, const mad_ved_stats& st) {
+  if (rc != MAD_OK || !st.stalled) return rc;
+  v->err = "tolerance not reached: the stall guard ended a diffusion step at relres " +
+           std::to_string(st.last_relres) + " (the storage precision's floor)";
+  return MAD_ERR_NOT_CONVERGED;
+}
+
 int mad_ved_run(mad_ved_ctx* v, const void* in, int32_t in_dtype, void* out, int32_t out_dtype,
                 mad_ved_stats* st) {
   if (!v || !in || !out) return MAD_ERR_INVALID;
-  return ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, false, st); });
+  mad_ved_stats local{};
+  mad_ved_stats* s = st ? st : &local;
+  return ved_run_status(v, ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, false, s); }), *s);
 }
 
 int mad_ved_run_device(mad_ved_ctx* v, const void* in, int32_t in_dtype, void* out,
                        int32_t out_dtype, mad_ved_stats* st) {
   if (!v || !in || !out) return MAD_ERR_INVALID;
-  return ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, true, st); });
+  mad_ved_stats local{};
+  mad_ved_stats* s = st ? st : &local;
+  return ved_run_status(v, ved_guarded(v, [&] { ved_run_impl(v, in, in_dtype, out, out_dtype, true, s); }), *s);
 }
 
 int mad_ved_comm_init(mad_ved_ctx* v, const void* uid128) {

@@ -81,7 +81,7 @@ class MultigridAnisotropicDiffusionImageFilter:
     VCYCLE, FMG, SMOOTHER = C.VCYCLE, C.FMG, C.SMOOTHER
 
     def __init__(self, smoother=MultigridGaussSeidelSmoother, output_dtype=np.float32,
-                 precision=C.FP32, device=-1):
+                 precision=C.PRECISION_AUTO, device=-1):
         self._smoother = smoother
         self._output_dtype = np.dtype(output_dtype)
         self._precision = precision

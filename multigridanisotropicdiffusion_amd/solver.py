@@ -58,7 +58,7 @@ class Solver:
     def __init__(self, shape, spacing=None, *, time_step=0.01, cycle=C.VCYCLE,
                  smoother=C.GAUSS_SEIDEL, iterations_per_grid=2, max_cycles=100,
                  number_of_steps=1, tolerance=1e-6, omega=2.0 / 3.0, verbose=False,
-                 precision=C.FP32, stall_guard=None, device=-1, tensor_kind=C.TENSOR_AUTO,
+                 precision=C.PRECISION_AUTO, stall_guard=None, device=-1, tensor_kind=C.TENSOR_AUTO,
                  nranks=1, rank=0, global_shape=None, gs_kernel=0):
         L = C.load()
         self.shape = tuple(int(s) for s in shape)  # this rank's slab
@@ -227,10 +227,12 @@ class Solver:
             raise ValueError(f"image shape {img.shape} != {self.shape}")
         out = np.empty(self.shape, dtype=out_dtype)
         st = C.MadStats()
-        self._check(self._L.mad_run(self._ctx, img.ctypes.data_as(ctypes.c_void_p),
-                                    mad_dtype(img.dtype), out.ctypes.data_as(ctypes.c_void_p),
-                                    mad_dtype(out_dtype), ctypes.byref(st)))
+        rc = C.check(self._L.mad_run(self._ctx, img.ctypes.data_as(ctypes.c_void_p),
+                                     mad_dtype(img.dtype), out.ctypes.data_as(ctypes.c_void_p),
+                                     mad_dtype(out_dtype), ctypes.byref(st)),
+                     self._ctx, warn_not_converged=True)
         stats = st.as_dict()
+        stats["converged"] = rc == C.OK
         stats["step_cycles"], stats["step_relres"] = [], []
         for s in range(st.steps):
             cy, rr = ctypes.c_uint32(), ctypes.c_double()
@@ -239,6 +241,26 @@ class Solver:
             stats["step_cycles"].append(cy.value)
             stats["step_relres"].append(rr.value)
         return out, stats
+
+    def cycle_trace(self):
+        """Per-cycle history of the last run (mad_get_cycle_trace): list of (time step,
+        relres after the cycle, seconds since the run started) -- the reference's BENCHMARK
+        trace (itkMultigridAnisotropicDiffusionImageFilter.hxx:147-151, 222-227)."""
+        n = ctypes.c_uint32()
+        self._check(self._L.mad_get_cycle_trace(self._ctx, 0, None, None, None, ctypes.byref(n)))
+        k = n.value
+        st = (ctypes.c_uint32 * max(k, 1))()
+        rr = (ctypes.c_double * max(k, 1))()
+        sec = (ctypes.c_double * max(k, 1))()
+        self._check(self._L.mad_get_cycle_trace(self._ctx, k, st, rr, sec, ctypes.byref(n)))
+        return [(st[q], rr[q], sec[q]) for q in range(k)]
+
+    @property
+    def resolved_precision(self):
+        """The precision mad_create resolved (PRECISION_AUTO -> FP32 or FP32_REFINE)."""
+        d = C.MadDesc()
+        self._check(self._L.mad_get_desc(self._ctx, ctypes.byref(d)))
+        return d.precision
 
     def bench_smooth(self, level, sweeps):
         t, k, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()

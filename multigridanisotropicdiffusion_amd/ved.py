@@ -26,7 +26,7 @@ class VED:
                  scales=(0.300, 0.482, 0.775, 1.245, 2.000), iterations=1,
                  diffusion_iterations=5, cycle=C.VCYCLE, time_step=0.1, tolerance=1e-6,
                  diffusion_iterations_per_grid=2, verbose=False, smoother=C.GAUSS_SEIDEL,
-                 precision=C.FP32, device=-1, nranks=1, rank=0, hessian="recursive"):
+                 precision=C.PRECISION_AUTO, device=-1, nranks=1, rank=0, hessian="recursive"):
         if len(shape) != 3:
             raise ValueError("VED is 3D (itkVEDMultigridImageFilter.h:46)")
         if len(scales) > C.VED_MAX_SCALES:
@@ -98,10 +98,13 @@ class VED:
         img = self._img(image)
         out = np.empty((self.slab[1] - self.slab[0],) + self.shape[1:], dtype=out_dtype)
         st = C.VedStats()
-        self._check(self._L.mad_ved_run(self._ctx, img.ctypes.data_as(ctypes.c_void_p),
-                                        mad_dtype(img.dtype), out.ctypes.data_as(ctypes.c_void_p),
-                                        mad_dtype(out_dtype), ctypes.byref(st)))
-        return out, st.as_dict()
+        rc = C.check(self._L.mad_ved_run(self._ctx, img.ctypes.data_as(ctypes.c_void_p),
+                                         mad_dtype(img.dtype), out.ctypes.data_as(ctypes.c_void_p),
+                                         mad_dtype(out_dtype), ctypes.byref(st)),
+                     self._ctx, warn_not_converged=True, last_error=self._L.mad_ved_last_error)
+        stats = st.as_dict()
+        stats["converged"] = rc == C.OK
+        return out, stats
 
     def tensor(self, image):
         """One tensor generation: (SoA tensor (6, z, y, x), max response (z, y, x))."""
@@ -130,7 +133,7 @@ class VEDMultigridImageFilter:
     VCYCLE, FMG, SMOOTHER = C.VCYCLE, C.FMG, C.SMOOTHER
 
     def __init__(self, smoother=MultigridGaussSeidelSmoother, output_dtype=None,
-                 precision=C.FP32, device=-1, hessian="recursive"):
+                 precision=C.PRECISION_AUTO, device=-1, hessian="recursive"):
         self._smoother = smoother
         self._output_dtype = output_dtype
         self._hessian = hessian

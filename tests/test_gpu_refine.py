@@ -26,13 +26,16 @@ def M():
     return mod
 
 
-def lena_run(M, precision, smoother, cycle):
+def lena_run(M, precision, smoother, cycle, with_solver=False):
     lena = np.load(os.path.join(GOLDEN, "lena_256_u8.npy")).astype(np.float64)
     T = np.stack([np.full(lena.shape, 50.0), np.zeros(lena.shape), np.full(lena.shape, 30.0)], axis=-1)
+    kw = {} if precision is None else dict(precision=precision)  # None: the descriptor default
     s = M.Solver(lena.shape, (1.0, 1.0), time_step=0.1, smoother=smoother, cycle=cycle,
-                 iterations_per_grid=2, max_cycles=100, tolerance=1e-10, precision=precision)
+                 iterations_per_grid=2, max_cycles=100, tolerance=1e-10, **kw)
     s.set_tensor(T)
     out, st = s.run(lena, out_dtype=np.float64)
+    if with_solver:
+        return out, st, s
     s.close()
     return out, st
 
@@ -80,9 +83,90 @@ def test_ved_parameters_reach_reference_tolerance(M, fixture, crop, spacing):
 
 def test_plain_fp32_stalls_where_refine_converges(M):
     """The contrast: plain fp32 ends at its rounding floor (stall guard) above 1e-10 on the
-    same C1 solve that the refined mode converges."""
-    out, st = lena_run(M, M.FP32, M.GAUSS_SEIDEL, M.VCYCLE)
-    assert st["last_relres"] > 1e-10 and st["stalled"]
+    same C1 solve that the refined mode converges -- and says so: mad_run returns
+    MAD_ERR_NOT_CONVERGED (a warning here, the output is written), never a silent early exit."""
+    with pytest.warns(M.NotConvergedWarning, match="tolerance 1e-10 not reached"):
+        out, st = lena_run(M, M.FP32, M.GAUSS_SEIDEL, M.VCYCLE)
+    assert st["last_relres"] > 1e-10 and st["stalled"] and not st["converged"]
+    assert np.isfinite(out).all()
+
+
+@pytest.mark.parametrize("smoother,cycle", [("WJ", "VCYCLE"), ("GS", "VCYCLE"), ("GS", "FMG")])
+def test_default_descriptor_reaches_reference_tolerance(M, smoother, cycle):
+    """a plain-default port of itk2DDiffusionTest (no precision given; the
+    descriptor default MAD_PRECISION_AUTO) at the reference's Tolerance 1e-10 resolves to the
+    fp64 defect correction and converges: relres <= 1e-10, no stall, status MAD_OK."""
+    import warnings
+    golden = load_golden("lena_c1_f64")
+    key = ("wj" if smoother == "WJ" else "gs") + ("_v" if cycle == "VCYCLE" else "_fmg")
+    sm = M.WEIGHTED_JACOBI if smoother == "WJ" else M.GAUSS_SEIDEL
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", M.NotConvergedWarning)
+        out, st, s = lena_run(M, None, sm, getattr(M, cycle), with_solver=True)
+    assert s.resolved_precision == M.FP32_REFINE
+    s.close()
+    assert st["converged"] and not st["stalled"] and st["last_relres"] <= 1e-10, st
+    assert relinf(out, golden[key]) < 1e-8
+
+
+def test_default_precision_resolution(M):
+    """MAD_PRECISION_AUTO: plain fp32 at tolerances fp32 storage resolves (>= 1e-6, the
+    reference default), the fp64 defect correction below; explicit choices are kept."""
+    shape = (16, 16, 16)
+    for tol, kw, want in [(1e-6, {}, M.FP32), (1e-4, {}, M.FP32), (1e-7, {}, M.FP32_REFINE),
+                          (1e-10, {}, M.FP32_REFINE), (1e-10, dict(precision=M.FP32), M.FP32),
+                          (1e-10, dict(precision=M.FP64), M.FP64)]:
+        s = M.Solver(shape, tolerance=tol, **kw)
+        assert s.resolved_precision == want, (tol, kw)
+        s.close()
+
+
+def test_default_ved_filter_reaches_reference_tolerance(M):
+    """itkVEDTest_GS's MAD parameters (Tolerance 1e-10) through the default descriptor on the
+    ved_test crop: every step converges to 1e-10 (no stall) and matches the fp64 oracle."""
+    v = np.load(os.path.join(GOLDEN, "ved_crop_i16.npy"))
+    golden = load_golden("ved_mad")
+    s = M.Solver(v.shape, (0.3125, 0.3125, 0.5), time_step=0.1, iterations_per_grid=3,
+                 number_of_steps=4, tolerance=1e-10)
+    s.set_tensor(synth.ved_form(v.shape))
+    out, st = s.run(v, out_dtype=np.float64)
+    s.close()
+    assert st["converged"] and not st["stalled"] and st["last_relres"] <= 1e-10, st
+    assert max(st["step_relres"]) <= 1e-10, st["step_relres"]
+    assert relinf(out, golden["out"]) < 1e-8
+
+
+def test_cycle_trace_matches_oracle_history(M, oracle_mod):
+    """mad_get_cycle_trace (the reference's BENCHMARK trace, MAD.hxx:147-151, 222-227): on the
+    C1 lena solve (fp64, WJ V-cycles, 2 time steps) the relres after every cycle equals the
+    oracle's cycle-by-cycle history (same algorithm, both fp64), and the clock only advances."""
+    lena = np.load(os.path.join(GOLDEN, "lena_256_u8.npy")).astype(np.float64)
+    T = np.stack([np.full(lena.shape, 50.0), np.zeros(lena.shape), np.full(lena.shape, 30.0)])
+    s = M.Solver(lena.shape, (1.0, 1.0), time_step=0.1, smoother=M.WEIGHTED_JACOBI,
+                 iterations_per_grid=2, tolerance=1e-10, number_of_steps=2, precision=M.FP64)
+    s.set_tensor(T)
+    out, st = s.run(lena, out_dtype=np.float64)
+    tr = s.cycle_trace()
+    s.close()
+    assert len(tr) == st["total_cycles"]
+    o = oracle_mod.Oracle(lena.shape, (1.0, 1.0), T, 0.1)
+    want = []
+    b = lena.copy()
+    for step in range(2):
+        x = b.copy()
+        bn = oracle_mod.l2norm(b)
+        while True:
+            x = o.vcycle(x, b, smoother=oracle_mod.WJ, iterations_per_grid=2)
+            rr = oracle_mod.l2norm(o.residual(0, x, b)) / bn
+            want.append((step, rr))
+            if rr <= 1e-10 or len(want) > 200:
+                break
+        b = x
+    assert [t[0] for t in tr] == [w[0] for w in want]
+    for (stp, rr, sec), (_, rw) in zip(tr, want):
+        assert abs(rr - rw) <= 1e-6 * rw + 1e-14, (stp, rr, rw)
+    secs = [t[2] for t in tr]
+    assert all(b2 >= a2 for a2, b2 in zip(secs, secs[1:])) and secs[0] > 0
 
 
 def test_refine_rank_slabs_match_single(M):
