@@ -587,8 +587,11 @@ const char* mad_ved_last_error(const mad_ved_ctx* v) { return v ? v->err.c_str()
 // as mad_run: MAD_ERR_NOT_CONVERGED (output written) when a diffusion step stalled above Tolerance
 static int ved_run_status(mad_ved_ctx* v, int rc, const mad_ved_stats& st) {
   if (rc != MAD_OK || !st.stalled) return rc;
-  v->err = "tolerance not reached: the stall guard ended a diffusion step at relres " +
-           std::to_string(st.last_relres) + " (the storage precision's floor)";
+  char buf[200];
+  std::snprintf(buf, sizeof buf,
+                "tolerance %g not reached: the stall guard ended a diffusion step at relres %g (the "
+                "storage precision's floor)", v->d.tolerance, st.last_relres);
+  v->err = buf;
   return MAD_ERR_NOT_CONVERGED;
 }
 
