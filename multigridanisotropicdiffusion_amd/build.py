@@ -11,8 +11,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmad_hip.so")
 SOURCES = ["mad_solver.hip"]
-DEPS = ["mad_solver.hip", "mad_kernels.hpp", "mad_comm.hpp", "mad_ved.hpp", "mad_ved_kernels.hpp",
-        "../../include/mad.h", "../../include/mad_ved.h"]
+DEPS = ["../../include/mad.h", "../../include/mad_ved.h"]
+
+
+def deps():
+    """every source the library is compiled from: csrc/*.hip, csrc/*.hpp and the C headers"""
+    return [f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp"))] + DEPS
 
 
 def hipcc():
@@ -26,7 +30,7 @@ def up_to_date():
     if not os.path.exists(OUT):
         return False
     t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(os.path.join(CSRC, d)) <= t for d in DEPS)
+    return all(os.path.getmtime(os.path.join(CSRC, d)) <= t for d in deps())
 
 
 def build(force=False, verbose=True):

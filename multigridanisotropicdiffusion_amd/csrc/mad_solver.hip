@@ -31,6 +31,7 @@
 #include "../../include/mad.h"
 #include "mad_comm.hpp"
 #include "mad_kernels.hpp"
+#include "mad_tsweep.hpp"
 
 using namespace mad;
 
@@ -268,6 +269,11 @@ struct LevelData {
   // as cf, no g): the fused sweep gs_fusedg_k reads these and recomputes g
   T* ct = nullptr;
   T* ct_alloc = nullptr;
+  // tensor array of the g-free level sweep gs_tsweep_k (build_gt_k: natural x order, TSweepGeom::PAD
+  // padding points per side with the domain-face ghosts, GHOST planes); gt = plane 0
+  T* gt = nullptr;
+  T* gt_alloc = nullptr;
+  TGeo tg{};
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -357,7 +363,8 @@ class Solver final : public SolverBase {
       // The full-tensor GS sweep (gs_fusedg_k) reads the dense b with its plane stream, so
       // it needs no record b.
       bool brec_on = c->d.cycle == MAD_SMOOTHER &&
-                     !(c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d));
+                     !(c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL &&
+                       (fusedg_wanted(c->d) || tsweep_level(c, l, L)));
       if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
       if (const char* e = std::getenv("MAD_BREC")) brec_on = e[0] != '0';
       L.brec = (dim == 3 && l == 0 && brec_on);
@@ -376,6 +383,17 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipMalloc(&L.ct_alloc, sizeof(T) * ttot));
         HIP_CHECK(hipMemsetAsync(L.ct_alloc, 0, sizeof(T) * ttot, c->stream));
         L.ct = L.ct_alloc + margin * 6 + cgp * tplane;
+      }
+      if (tsweep_level(c, l, L)) {
+        using TG = TSweepGeom;
+        const int64_t ntx = (L.g.nx + TG::TX - 1) / TG::TX, nty = (L.g.ny + TG::TY - 1) / TG::TY;
+        L.tg.tpitch = ntx * TG::TX + 2 * TG::PAD;
+        L.tg.trow = TG::NCOMP * L.tg.tpitch;
+        L.tg.tplane = (nty * TG::TY + 2 * TG::PAD) * L.tg.trow;
+        const int64_t ttot = (L.g.nz + 2 * (int64_t)GHOST) * L.tg.tplane;
+        HIP_CHECK(hipMalloc(&L.gt_alloc, sizeof(T) * ttot));
+        HIP_CHECK(hipMemsetAsync(L.gt_alloc, 0, sizeof(T) * ttot, c->stream));
+        L.gt = L.gt_alloc + (int64_t)GHOST * L.tg.tplane;
       }
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
@@ -629,6 +647,41 @@ class Solver final : public SolverBase {
   bool fusedg_on(const LevelData<T>& L) const {
     return L.ct != nullptr && c_->kind == KFULL && fusedg_wanted(c_->d);
   }
+  // the g-free level sweep gs_tsweep_k (fp32 full tensor; 36 instead of 48 B per voxel-sweep):
+  // gs_kernel 7, on the levels the fused sweep runs (3D, >= 4 M voxels, >= 64 planes)
+  static bool tsweep_level(const mad_ctx* c, int l, const LevelData<T>& L) {
+    (void)l;
+    if (!(sizeof(T) == 4 && c->dim == 3 && c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL))
+      return false;
+    if (c->d.gs_kernel == 7) return true;  // every 3D level (parity tests)
+    return false;
+  }
+  bool tsweep_on(const LevelData<T>& L) const { return L.gt != nullptr; }
+  void launch_tsweep(LevelData<T>& L, int part) {
+    if constexpr (sizeof(T) == 4) {
+      using TG = TSweepGeom;
+      const int ntx = (L.g.nx + TG::TX - 1) / TG::TX, nty = (L.g.ny + TG::TY - 1) / TG::TY;
+      const int tiles = ntx * nty;
+      FusedCfg fc;
+      fc.blocks = 256;  // one workgroup per CU (155 KB of LDS), one round
+      int flip = 0;
+      uint32_t* sig = nullptr;
+      const ZRange zr = part_range(L, tiles, fc, part, &flip, &sig);
+      REQUIRE(flip == 0 && sig == nullptr, MAD_ERR_UNSUPPORTED, "gs_tsweep_k marches upward only");
+      static bool attr = false;
+      if (!attr) {
+        HIP_CHECK(hipFuncSetAttribute((const void*)gs_tsweep_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      TG::LDS_BYTES));
+        attr = true;
+      }
+      hipLaunchKernelGGL(gs_tsweep_k, dim3((unsigned)(tiles * zr.nchunks)), dim3(TG::NT), TG::LDS_BYTES,
+                         c_->stream, L.x, L.t, L.b, L.gt, L.g, L.tg, zr.zc, ntx, nty, zr.zbase, zr.zstride);
+    } else {
+      (void)L;
+      (void)part;
+      throw MadError(MAD_ERR_UNSUPPORTED, "gs_tsweep_k is fp32 only");
+    }
+  }
   // gs_fusedg_k tile: fp32 64x16 (432 blocks of 2x2 points, 512 threads, 2 waves per
   // SIMD for ~200 VGPRs of records in flight), 32x32 (MAD_FUSEDG_TILE=1) or 32x16 on 256
   // threads, two workgroups per CU (MAD_FUSEDG_TILE=2); fp64 32x16 on 256 threads (one wave
@@ -785,6 +838,13 @@ class Solver final : public SolverBase {
 
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
   void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {
+    if (tsweep_on(L)) {
+      FusedCfg fc;
+      fc.blocks = 256;
+      *tiles = ((L.g.nx + TSweepGeom::TX - 1) / TSweepGeom::TX) * ((L.g.ny + TSweepGeom::TY - 1) / TSweepGeom::TY);
+      *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
+      return;
+    }
     if (fusedg_on(L)) {
       int tx, ty, nt;
       fusedg_dims(&tx, &ty, &nt);
@@ -808,7 +868,10 @@ class Solver final : public SolverBase {
 
   void launch_fused_part(LevelData<T>& L, int part, bool prolong = false) {
     const FusedCfg& fc = fused_cfg();
-    if (fusedg_on(L)) {
+    if (tsweep_on(L)) {
+      REQUIRE(!prolong, MAD_ERR_STATE, "prolongation fold: not with gs_tsweep_k");
+      launch_tsweep(L, part);
+    } else if (fusedg_on(L)) {
       if constexpr (sizeof(T) == 8) {
         launch_fusedg<32, 16, 256>(L, part);
       } else {
@@ -855,6 +918,9 @@ class Solver final : public SolverBase {
     } else if (c_->d.gs_kernel == 2) {
       std::snprintf(buf, sizeof buf, "gs_fused_k<%s, %d, 64, 16, %d, %d>", tn, kind,
                     kind == KFULL ? 512 : 1024, sizeof(T) == 8 ? 2 : 4);
+    } else if (tsweep_on(lv_[l])) {
+      std::snprintf(buf, sizeof buf, "gs_tsweep_k");
+      if (sweep_overlap(l)) return std::string(buf) + " [rank slab: boundary + interior launches]";
     } else if (fusedg_on(lv_[l])) {
       int tx, ty, nt;
       fusedg_dims(&tx, &ty, &nt);
@@ -948,7 +1014,7 @@ class Solver final : public SolverBase {
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
-    if (L.brec && c_->d.gs_kernel != 2 && !fusedg_on(L)) {
+    if (L.brec && c_->d.gs_kernel != 2 && !fusedg_on(L) && !tsweep_on(L)) {
       sync_brec(l);
     } else if (!L.b_halo_ok) {
       halo(l, L.b, GHOST);
@@ -1671,7 +1737,8 @@ class Solver final : public SolverBase {
     const int def_tile = sizeof(T) == 4 ? 1 : 0;
     return env && c_->dim == 3 && !c_->comm.active() && !c_->d.verbose && c_->kind == KFULL &&
            c_->d.smoother == MAD_GAUSS_SEIDEL && (c_->d.gs_kernel == 0 || c_->d.gs_kernel == 3) &&
-           c_->d.iterations_per_grid >= 1 && use_fused(l) && !fusedg_on(lv_[l]) && !lv_[l].brec &&
+           c_->d.iterations_per_grid >= 1 && use_fused(l) && !fusedg_on(lv_[l]) && !tsweep_on(lv_[l]) &&
+           !lv_[l].brec &&
            fc.tile == def_tile;
   }
   void fmg() override { fmg_rec(0); }
@@ -2072,6 +2139,7 @@ class Solver final : public SolverBase {
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
       if (L.ct_alloc) (void)hipFree(L.ct_alloc);
+      if (L.gt_alloc) (void)hipFree(L.gt_alloc);
     }
     lv_.clear();
     for (auto& a : r64alloc_)
@@ -2244,6 +2312,14 @@ class Solver final : public SolverBase {
           HIP_CHECK(hipStreamSynchronize(c_->stream));
           HIP_CHECK(hipFree(full64));
         }
+      }
+      if (L.gt) {
+        // the g-free sweep's tensor array (with the face ghosts) from the finished records
+        const int p0 = -GHOST, p1 = L.g.nz + GHOST;
+        dim3 grt((unsigned)((L.g.nx + 2 + 63) / 64), (unsigned)((L.g.ny + 2 + 3) / 4), (unsigned)(p1 - p0));
+        if constexpr (sizeof(T) == 4)
+          hipLaunchKernelGGL((build_gt_k<T>), grt, BLK, 0, c_->stream, L.cf, L.g, L.gt, L.tg, p0);
+        HIP_CHECK(hipGetLastError());
       }
       if (L.ct) {
         // tensor records of every allocated plane the coefficient records hold

@@ -185,14 +185,16 @@ def test_fused_gs_sweep_is_bitwise_per_colour_passes(shape, tensor, prec, cycle)
     and 3-point axes (both mirror images of one point); so does v3 with its last
     z-chunk run on the z-reflected view (the rank-slab single-launch form), and so do
     gs_kernel 5 / 6 (gs_fusedg_k: g recomputed in-kernel from tensor records, one-sided
-    differences at the x/y/z faces; non-full tensors fall back to v3)."""
+    differences at the x/y/z faces; non-full tensors fall back to v3), and gs_kernel 7
+    (gs_tsweep_k: the g-free sweep reading the 24-B tensor with face ghosts; fp32 full tensor,
+    else v3)."""
     import multigridanisotropicdiffusion_amd as M
     import synth
     T = {"full": lambda: synth.random_spd(shape, seed=1),
          "diag": lambda: synth.random_spd(shape, seed=1, offdiag=False),
          "iso": lambda: synth.isotropic(shape)}[tensor]()
     outs = []
-    for variant in (1, 2, 3, 4, 5, 6):  # 4 / 6: the last z-chunk marched downward
+    for variant in (1, 2, 3, 4, 5, 6, 7):  # 4 / 6: the last z-chunk marched downward
         s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec, gs_kernel=variant,
                      cycle=cycle)
         s.set_tensor(T)
