@@ -474,20 +474,32 @@ __device__ __forceinline__ void tsweep_body(const float* __restrict__ uin, float
         }
       }
       if (plane_ok(k + 1)) uput(k + 1);
+#ifndef TSW_PROBE_NO_FORM
       form(u & 1, rec[u]);
+#endif
+#ifndef TSW_PROBE_NO_ULOAD
       uload(k + 2);
       bload(k + 1);
+#endif
       tsweep_barrier();
       // phase 2k; tensor plane k+2 into the buffer plane k leaves (everyone formed plane k)
+#ifndef TSW_PROBE_NO_TLOAD  // measurement builds only (tools/probe_tsweep.sh)
       tload(k + 2, u & 1);
+#endif
+#ifndef TSW_PROBE_NO_STAGE
       instance(0, k, u);
       instance(2, k - 1, (u + U - 1) % U);
+#endif
       tsweep_barrier();
       // phase 2k+1
+#ifndef TSW_PROBE_NO_STAGE
       instance(1, k, u);
       instance(3, k - 1, (u + U - 1) % U);
+#endif
       // this iteration's loads (and the stores, issued three phases ago) have landed
+#ifndef TSW_PROBE_NO_WAIT
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
       tsweep_barrier();
     }
   }
