@@ -116,15 +116,18 @@ typedef struct mad_desc {
   int32_t tensor_kind;           /* mad_tensor_kind, default AUTO */
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
   int32_t rank;                  /* this rank */
-  int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep, v3),
-                                    1 one launch per colour, 2 fused v2, 3 fused v3,
-                                    4 fused v3 with the last z-chunk marched downward (the
-                                    rank-slab form, selectable on one GPU for parity),
-                                    5 / 6 as 3 / 4 with g recomputed in-kernel from 24-B
-                                    tensor records (full tensor only; gs_fusedg_k: fewer
-                                    bytes, but latency-bound and slower today) */
-  int32_t reserved[8];
+  int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep
+                                    gs_fused3_k on large levels, one launch per colour below),
+                                    1 one launch per colour, 3 gs_fused3_k, 4 gs_fused3_k with
+                                    the last z-chunk marched downward (the rank-slab single-
+                                    launch form, selectable on one GPU for parity) */
+  uint32_t options;              /* MAD_OPT_* bits, default 0 */
+  int32_t reserved[7];
 } mad_desc;
+
+/* mad_desc.options: MAD_OPT_EAGER_RANK_VCYCLE keeps a multi-rank V-cycle eager instead of
+   replaying its captured hipGraph (the reference of the graph-replay parity test) */
+#define MAD_OPT_EAGER_RANK_VCYCLE 1u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

@@ -64,8 +64,14 @@ typedef struct mad_ved_desc {
                                       reference's HessianRecursiveGaussianImageFilter operator,
                                       VED.hxx:158-173) or MAD_VED_HESSIAN_FIR (sampled Gaussian
                                       derivative taps, round 1) */
-  int32_t reserved[5];
+  uint32_t options;                /* MAD_VED_OPT_* bits, default 0 */
+  int32_t reserved[4];
 } mad_ved_desc;
+
+/* mad_ved_desc.options: MAD_VED_OPT_LINE_WALK runs the recursive Hessian as one thread per
+   line and output for every axis (ved_iir_k, the slow parity reference of the production passes,
+   which equal it bit for bit) */
+#define MAD_VED_OPT_LINE_WALK 1u
 
 typedef enum mad_ved_hessian_kind {
   MAD_VED_HESSIAN_RECURSIVE = 0,

@@ -29,6 +29,9 @@ VED_HESSIAN_RECURSIVE, VED_HESSIAN_FIR = 0, 1
 TENSOR_AUTO, TENSOR_ISOTROPIC, TENSOR_DIAGONAL, TENSOR_FULL = range(4)
 # mad_which
 X, B, R = 0, 1, 2
+# mad_desc.options / mad_ved_desc.options
+OPT_EAGER_RANK_VCYCLE = 1
+VED_OPT_LINE_WALK = 1
 
 EXPORTS = (
     "mad_desc_init", "mad_max_depth", "mad_create", "mad_destroy", "mad_last_error",
@@ -72,7 +75,8 @@ class MadDesc(ctypes.Structure):
         ("nranks", ctypes.c_int32),
         ("rank", ctypes.c_int32),
         ("gs_kernel", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 8),
+        ("options", ctypes.c_uint32),
+        ("reserved", ctypes.c_int32 * 7),
     ]
 
 
@@ -122,7 +126,8 @@ class VedDesc(ctypes.Structure):
         ("nranks", ctypes.c_int32),
         ("rank", ctypes.c_int32),
         ("hessian", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 5),
+        ("options", ctypes.c_uint32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 

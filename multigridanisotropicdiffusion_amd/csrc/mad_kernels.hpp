@@ -343,18 +343,8 @@ __device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t r, uint32_
 }
 
 // one coefficient record (NCF values of T) at byte offset voff: dword x3 chunks when
-// the record is a multiple of 12 bytes, else x4 chunks + remainder
-// cache policy of the fused sweep's streams (aux bits of the buffer instructions;
-// 2 = nt).  Default policy unless a measurement build overrides them.
-#ifndef MAD_REC_AUX
-#define MAD_REC_AUX 0
-#endif
-#ifndef MAD_U_AUX
-#define MAD_U_AUX 0
-#endif
-#ifndef MAD_ST_AUX
-#define MAD_ST_AUX 0
-#endif
+// the record is a multiple of 12 bytes, else x4 chunks + remainder (default cache policy:
+// the nt policy measured 1.04-1.9x slower on these streams, profiles/r01_policy_ab.log)
 
 template <typename T, int NCF>
 __device__ __forceinline__ void buf_load_rec(__amdgpu_buffer_rsrc_t r, uint32_t voff, T* out) {
@@ -365,24 +355,24 @@ __device__ __forceinline__ void buf_load_rec(__amdgpu_buffer_rsrc_t r, uint32_t 
   if constexpr (NB % 12 == 0 && NB % 16 != 0) {
 #pragma unroll
     for (int q = 0; q < NW / 3; ++q) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 12 * q, MAD_REC_AUX);
+      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 12 * q, 0);
       w[3 * q] = v[0]; w[3 * q + 1] = v[1]; w[3 * q + 2] = v[2];
     }
   } else {
     int q = 0;
 #pragma unroll
     for (; q + 4 <= NW; q += 4) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 4 * q, MAD_REC_AUX);
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 4 * q, 0);
       w[q] = v[0]; w[q + 1] = v[1]; w[q + 2] = v[2]; w[q + 3] = v[3];
     }
     if constexpr (NW % 4 == 3) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 4 * (NW - 3), MAD_REC_AUX);
+      auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, 4 * (NW - 3), 0);
       w[NW - 3] = v[0]; w[NW - 2] = v[1]; w[NW - 1] = v[2];
     } else if constexpr (NW % 4 == 2) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 4 * (NW - 2), MAD_REC_AUX);
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 4 * (NW - 2), 0);
       w[NW - 2] = v[0]; w[NW - 1] = v[1];
     } else if constexpr (NW % 4 == 1) {
-      w[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 4 * (NW - 1), MAD_REC_AUX);
+      w[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 4 * (NW - 1), 0);
     }
   }
   __builtin_memcpy(out, w, NB);
@@ -403,204 +393,10 @@ struct FusedGeom {
   static constexpr int cols(int c) { return (TX + 2 * (NC - 1 - c)) / 2; }
 };
 
-template <typename T, int KIND, int TX, int TY, int NT, int MINW>
-__global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin, T* __restrict__ uout,
-                                                       const T* __restrict__ b, const T* __restrict__ cf,
-                                                       Geo g, Rat<T> rat, int zc, int ntx, int nty) {
-  constexpr int NC = (KIND == KFULL) ? 4 : 2;
-  using FG = FusedGeom<NC, TX, TY>;
-  constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
-  constexpr int PLANE = FG::PLANE, NP = FG::NP;
-  constexpr int UPT = (RX * RY + NT - 1) / NT;
-  constexpr int OPT = (TX * TY + NT - 1) / NT;
-  constexpr int NCF = CoefLayout<3, KIND>::N;
-  constexpr int NNB = NbCount<3, KIND>::N;
-  static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
-  static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
-  __shared__ T lds[NP * PLANE];
-
-  // XCD-aware, bijective block -> (chunk, tile): the tiles of one chunk share an XCD (L2)
-  int bid = blockIdx.x;
-  {
-    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = bid & 7, idx = bid >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int tiles = ntx * nty;
-  const int chunk = bid / tiles;
-  const int tile = bid - chunk * tiles;
-  const int tyi = tile / ntx;
-  const int txi = tile - tyi * ntx;
-  const int rx0 = txi * TX - H;
-  const int ry0 = tyi * TY - H;
-  const int tid = threadIdx.x;
-  const int nx = g.nx, ny = g.ny, sy = (int)g.sy;
-  const int64_t sz = g.sz;
-
-  const int zlo = g.zlo_ghost ? -GHOST : 0;          // loadable planes [zlo, zhi)
-  const int zhi = g.zhi_ghost ? g.nz + GHOST : g.nz;
-  const int ulo = g.zlo_ghost ? -(GHOST - 1) : 0;    // updatable planes [ulo, uhi)
-  const int uhi = g.zhi_ghost ? g.nz + GHOST - 1 : g.nz;
-  const int z0 = chunk * zc;
-  const int z1 = min(z0 + zc, g.nz);
-  const int kbeg = z0 - (NC - 1);
-  const int kend = z1 + NC - 2;
-
-  // ---- per-thread constants (hoisted out of the z loop)
-  // region plane elements handled by this thread for loads: LDS index + in-plane offset
-  int u_lds[UPT], u_off[UPT];
-#pragma unroll
-  for (int e = 0; e < UPT; ++e) {
-    const int q = tid + e * NT;
-    const int lj = q / RX, li = q - (q / RX) * RX;
-    const int gi = rx0 + li, gj = ry0 + lj;
-    const bool ok = q < RX * RY && gi >= 0 && gi < nx && gj >= 0 && gj < ny;
-    u_lds[e] = ok ? lj * PITCH + (li & 1) * HALF + (li >> 1) : -1;
-    u_off[e] = gj * sy + gi;
-  }
-  // stage point (r, t) of this thread, per stage
-  int st_r[NC], st_t[NC];
-  bool st_has[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int cols = FG::cols(c);
-    st_has[c] = tid < FG::rows(c) * cols;
-    st_r[c] = tid / cols;
-    st_t[c] = tid - (tid / cols) * cols;
-  }
-  auto slot = [](int m) { return (m + NP * 64) % NP; };
-  auto plane_ok = [&](int m) { return m >= zlo && m < zhi; };
-  auto stage_on = [&](int c, int m) {
-    const int h = NC - 1 - c;
-    return m >= z0 - h && m < z1 + h && m >= ulo && m < uhi;
-  };
-  // (li, lj) of this thread's stage-c point on plane m
-  auto locate = [&](int c, int m, int& li, int& lj) -> bool {
-    const int h = NC - 1 - c;
-    const int l0 = H - h;
-    const int pm = (m + g.zoff) & 1;
-    if (NC == 4) {
-      lj = l0 + ((((c >> 1) ^ pm ^ l0) & 1)) + 2 * st_r[c];
-      li = l0 + (((c & 1) ^ pm ^ l0) & 1) + 2 * st_t[c];
-    } else {
-      lj = l0 + st_r[c];
-      li = l0 + ((c ^ pm ^ lj ^ l0) & 1) + 2 * st_t[c];
-    }
-    const int gi = rx0 + li, gj = ry0 + lj;
-    return st_has[c] && gi >= 0 && gi < nx && gj >= 0 && gj < ny;
-  };
-
-  T up[UPT];
-  T raw[NC][NCF];
-  T bv[NC];
-  auto load_plane = [&](int m) {
-    const T* base = uin + (int64_t)m * sz;
-#pragma unroll
-    for (int e = 0; e < UPT; ++e) up[e] = (u_lds[e] >= 0) ? base[u_off[e]] : T(0);
-  };
-  auto put_plane = [&](int m) {
-    T* P = lds + slot(m) * PLANE;
-#pragma unroll
-    for (int e = 0; e < UPT; ++e)
-      if (u_lds[e] >= 0) P[u_lds[e]] = up[e];
-  };
-  auto load_stage = [&](int c, int k) {
-    const int m = k - c;
-    int li, lj;
-    if (stage_on(c, m) && locate(c, m, li, lj)) {
-      const int gi = rx0 + li, gj = ry0 + lj;
-      const T* cp = cf + (int64_t)m * sz * g.rs;
-      const int co = gj * sy + ((gi & 1) ? g.hx0 + (gi >> 1) : (gi >> 1));
-#pragma unroll
-      for (int a = 0; a < NCF; ++a) raw[c][a] = cp[(int64_t)co * g.rs + a];
-      bv[c] = b[(int64_t)m * sz + gj * sy + gi];
-    }
-  };
-
-  // prologue: planes kbeg-1, kbeg into LDS; plane kbeg+1 and step kbeg's stage data
-  for (int m = kbeg - 1; m <= kbeg; ++m)
-    if (plane_ok(m)) {
-      load_plane(m);
-      put_plane(m);
-    }
-  if (plane_ok(kbeg + 1)) load_plane(kbeg + 1);
-#pragma unroll
-  for (int c = 0; c < NC; ++c) load_stage(c, kbeg);
-
-  for (int k = kbeg; k <= kend; ++k) {
-    if (plane_ok(k + 1)) put_plane(k + 1);
-    if (k + 1 <= kend && plane_ok(k + 2)) load_plane(k + 2);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int m = k - c;
-      int li, lj;
-      if (stage_on(c, m) && locate(c, m, li, lj)) {
-        const int gi = rx0 + li, gj = ry0 + lj;
-        const int zm = (m == 0 && !g.zlo_ghost) ? 1 : m - 1;
-        const int zp = (m == g.nz - 1 && !g.zhi_ghost) ? g.nz - 2 : m + 1;
-        T* P0 = lds + slot(m) * PLANE;
-        const T* Pm = lds + slot(zm) * PLANE;
-        const T* Pp = lds + slot(zp) * PLANE;
-        const int il = lj * PITCH + (li & 1) * HALF + (li >> 1);
-        // split-row offsets of li +- 1 (the other parity half), mirrored at the border
-        const int ox_p = (li & 1) ? 1 - HALF : HALF;
-        const int ox_m = (li & 1) ? -HALF : HALF - 1;
-        const int oxp = (gi == nx - 1) ? ox_m : ox_p;
-        const int oxm = (gi == 0) ? ox_p : ox_m;
-        const int oyp = (gj == ny - 1) ? -PITCH : PITCH;
-        const int oym = (gj == 0) ? PITCH : -PITCH;
-        T nb[18];
-        nb[0] = P0[il + oxp];
-        nb[1] = P0[il + oxm];
-        nb[2] = P0[il + oyp];
-        nb[3] = P0[il + oym];
-        nb[4] = Pp[il];
-        nb[5] = Pm[il];
-        if (NNB == 18) {
-          nb[6] = P0[il + oxp + oyp];
-          nb[7] = P0[il + oxp + oym];
-          nb[8] = P0[il + oxm + oyp];
-          nb[9] = P0[il + oxm + oym];
-          nb[10] = Pp[il + oxp];
-          nb[11] = Pm[il + oxp];
-          nb[12] = Pp[il + oxm];
-          nb[13] = Pm[il + oxm];
-          nb[14] = Pp[il + oyp];
-          nb[15] = Pm[il + oyp];
-          nb[16] = Pp[il + oym];
-          nb[17] = Pm[il + oym];
-        }
-        Coefs<T> q;
-        coefs_from_raw<T, 3, KIND>(raw[c], rat, q);
-        const T bc = bv[c];
-        T D, S;
-        stencil_combine<T, 3, KIND>(q, nb, D, S);
-        P0[il] = gs_update(bc, S, D);
-      }
-      // this stage's registers are free: prefetch its data for the next step
-      if (k + 1 <= kend) load_stage(c, k + 1);
-      __syncthreads();
-    }
-    // plane k-NC+1 is final on the tile: store it (coalesced rows)
-    const int mo = k - NC + 1;
-    if (mo >= z0 && mo < z1) {
-      const T* P = lds + slot(mo) * PLANE;
-      T* out = uout + (int64_t)mo * sz;
-#pragma unroll
-      for (int e = 0; e < OPT; ++e) {
-        const int q = tid + e * NT;
-        const int lj = H + q / TX, li = H + (q - (q / TX) * TX);
-        const int gi = rx0 + li, gj = ry0 + lj;
-        if (q < TX * TY && gi < nx && gj < ny) out[gj * sy + gi] = P[lj * PITCH + (li & 1) * HALF + (li >> 1)];
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// Fused multicolour GS sweep, v3: same wavefront / overlapped-tile schedule and the
-// same arithmetic as gs_fused_k (bit-identical results), restructured so the
-// per-step instruction stream is almost free of address arithmetic:
+// Fused multicolour GS sweep, v3: the wavefront / overlapped-tile schedule above and the
+// same arithmetic as the per-colour passes (bit-identical results), with a per-step
+// instruction stream almost free of address arithmetic:
 //  * the x/y mirror boundary lives in the LDS tile: ghost positions at distance 1
 //    outside the domain hold mirror copies (loaded mirrored, and rewritten when
 //    their source point is updated), so every neighbour read is a ds_read with a
@@ -623,29 +419,13 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused_k(const T* __restrict__ uin
 // edge chunks then count themselves in sig[0] (bottom) / sig[1] (top), and the
 // communication stream, waiting on those counters, exchanges the halo while the rest
 // of the sweep runs -- one launch per sweep instead of boundary + interior launches.
-//
-// PROLONG (the V-cycle's first post-smoothing sweep, one rank): the sweep reads
-// x + P e_c instead of x -- the coarse-grid correction (MAD.hxx:422-435) folded into the
-// plane loads, with interp3_k's taps and arithmetic, so the result is bit-identical to
-// interp3_k followed by the sweep and level 0 skips interp3_k's x read-modify-write.  The
-// coarse planes the region's taps reach go through a 4-slot LDS ring after the fine ring,
-// one coarse plane loaded a step ahead.
-template <typename W>
-__device__ __forceinline__ void itaps2(int f, int nc, int cell, int* idx, W* w);  // (below)
 
-template <typename T>
-struct ProlongArgs {
-  const T* ec;  // coarse x (level l+1, dense; its sizes follow from the fine ones and the centring)
-  int cent;     // coarse centring flags (C.cent): x | y << 1 | z << 2
-};
-
-template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false,
-          bool PROLONG = false>
+template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
                                                         int zbase, int zstride, int flip_last,
-                                                        uint32_t* __restrict__ sig, ProlongArgs<T> pa) {
+                                                        uint32_t* __restrict__ sig) {
   constexpr int NC = (KIND == KFULL) ? 4 : 2;
   using FG = FusedGeom<NC, TX, TY>;
   constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
@@ -724,7 +504,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   // a quarter of the issue-bound sweep's vector instructions.  -1 marks no element.
   uint32_t usrc[UPT];
   int udst[UPT];
-  uint32_t ucrd[PROLONG ? UPT : 1];  // PROLONG: the element's (mirrored) fine x | y << 16
 #pragma unroll
   for (int e = 0; e < UPT; ++e) {
     const int q = tid + e * NT;
@@ -736,11 +515,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     }
     usrc[e] = (uint32_t)(gj * sy + gi) * TS;
     udst[e] = (q < RX * RY) ? (int)((lj * PITCH + (li & 1) * HALF + (li >> 1)) * TS) : -1;
-    // (clamped into the region too: only positions 2+ outside the domain change, whose values
-    // no stage point reads, and every tap then stays inside the coarse tile)
-    if constexpr (PROLONG)
-      ucrd[e] = (uint32_t)min(max(gi, max(rx0, 0)), min(rx0 + RX - 1, nx - 1)) |
-                ((uint32_t)min(max(gj, max(ry0, 0)), min(ry0 + RY - 1, ny - 1)) << 16);
   }
   int olds[OPT], oglb[OPT];
 #pragma unroll
@@ -826,84 +600,14 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   auto load_plane = [&](int m) {
     m = min(max(m, zlo), zhi - 1);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
-#ifdef MAD_PROBE_NO_U  // measurement builds only: drop the solution-plane stream
-    (void)rs;
 #pragma unroll
-    for (int e = 0; e < UPT; ++e) up[e] = T(0);
-#else
-#pragma unroll
-    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T, MAD_U_AUX>(rs, usrc[e], 0u);
-#endif
-  };
-  // ---- PROLONG: coarse tile (region's taps), 4-slot ring after the fine ring
-  constexpr int CXW = RX / 2 + 3, CYW = RY / 2 + 3, CPL = CXW * CYW;
-  constexpr int CPT = PROLONG ? (CPL + NT - 1) / NT : 1;  // coarse tile elements per thread
-  T* cring = reinterpret_cast<T*>(fused_smem + (size_t)NP * PLANE * TS);
-  const int ccx0 = (rx0 >> 1) - 1, ccy0 = (ry0 >> 1) - 1;  // coarse tile origin (floor)
-  uint32_t csrc[CPT];
-  T creg[CPT];
-  int chi = -1;  // highest coarse plane put into the ring
-  // coarse sizes: a cell-centred axis halves, a vertex-centred one keeps both ends
-  const int pcx = pa.cent & 1, pcy = (pa.cent >> 1) & 1, pcz = (pa.cent >> 2) & 1;
-  const int cnx = pcx ? nx / 2 : (nx + 1) / 2, cny = pcy ? ny / 2 : (ny + 1) / 2;
-  const int cnz = pcz ? g.nz / 2 : (g.nz + 1) / 2;
-  const int64_t csz = (int64_t)cnx * cny;
-#pragma unroll
-  for (int q = 0; q < CPT; ++q) {
-    csrc[q] = 0u;
-    creg[q] = T(0);
-    if constexpr (PROLONG) {
-      const int ce = min(tid + q * NT, CPL - 1);
-      const int lcy = ce / CXW, lcx = ce - (ce / CXW) * CXW;
-      csrc[q] = (uint32_t)(min(max(ccy0 + lcy, 0), cny - 1) * cnx + min(max(ccx0 + lcx, 0), cnx - 1)) * TS;
-    }
-  }
-  auto cload = [&](int K) {
-    const __amdgpu_buffer_rsrc_t rc = buf_rsrc(pa.ec + (int64_t)min(max(K, 0), cnz - 1) * csz);
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) creg[q] = buf_load<T>(rc, csrc[q], 0u);
-  };
-  auto cput = [&](int K) {
-#pragma unroll
-    for (int q = 0; q < CPT; ++q)
-      if (tid + q * NT < CPL) cring[(K & 3) * CPL + tid + q * NT] = creg[q];
-  };
-  // the coarse planes fine plane m's taps reach: up to (m >> 1) + 1 (clamped)
-  auto ctop = [&](int m) { return min(max(m + g.zoff, 0) / 2 + 1, cnz - 1); };
-  // x + P e_c at element e of fine plane m (interp3_k's taps and fma order)
-  auto prolong = [&](int e, int m, T xc) -> T {
-#pragma clang fp contract(off)
-    const int gi = (int)(ucrd[e] & 0xffffu), gj = (int)(ucrd[e] >> 16);
-    int ix[2], iy[2], iz[2];
-    T wx[2], wy[2], wz[2];
-    itaps2<T>(gi, cnx, pcx, ix, wx);
-    itaps2<T>(gj, cny, pcy, iy, wy);
-    itaps2<T>(m + g.zoff, cnz, pcz, iz, wz);
-    T v = T(0);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const T* pl = cring + (iz[c] & 3) * CPL - ccx0;
-      T vz = T(0);
-#pragma unroll
-      for (int bq = 0; bq < 2; ++bq) {
-        const T* row = pl + (iy[bq] - ccy0) * CXW;
-        vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
-      }
-      v = fma(wz[c], vz, v);
-    }
-    return xc + v;
+    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, usrc[e], 0u);
   };
   auto put_plane = [&](int m) {
     unsigned char* P = lbytes + slot(m) * (PLANE * TS);
 #pragma unroll
     for (int e = 0; e < UPT; ++e) {
-      if (e < UPT - 1 || udst[e] >= 0) {
-        T val = up[e];
-        if constexpr (PROLONG) val = prolong(e, m, val);
-        *reinterpret_cast<T*>(P + udst[e]) = val;
-      }
-      // one element at a time: the sweep has few registers to spare
-      if constexpr (PROLONG) __builtin_amdgcn_sched_barrier(0);
+      if (e < UPT - 1 || udst[e] >= 0) *reinterpret_cast<T*>(P + udst[e]) = up[e];
     }
   };
   // stage c data of step k (plane m = k - c, parity PM)
@@ -915,13 +619,8 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       const PD d = pdelta(c, PM);
       buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * RS), pg[c][PM % NPM],
                           raw[c]);
-      if constexpr (!BREC) {
-#ifdef MAD_PROBE_NO_B  // measurement builds only (tools/probe_builds.sh): drop the rhs stream
-        bv[c] = T(0);
-#else
+      if constexpr (!BREC)
         bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
-#endif
-      }
     }
   };
   auto stage = [&](int c, int k, int PM) {
@@ -997,17 +696,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   };
 
   // prologue: planes kbeg-1, kbeg into LDS; plane kbeg+1 and step kbeg's stage data
-  if constexpr (PROLONG) {
-    // coarse planes of fine planes kbeg-1 .. kbeg+1 (the puts of the prologue and step kbeg)
-    const int c0 = max(max(kbeg - 1 + g.zoff, 0) / 2 - 1, 0), c1 = ctop(kbeg + 1);
-    for (int K = c0; K <= c1; ++K) {
-      cload(K);
-      cput(K);
-    }
-    chi = c1;
-    if (chi + 1 <= ctop(kbeg + 2)) cload(chi + 1);
-    __syncthreads();
-  }
   for (int m = kbeg - 1; m <= kbeg; ++m)
     if (plane_ok(m)) {
       load_plane(m);
@@ -1026,14 +714,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
         // (stage, parity, flag) test out of the loop as a 64-bit lane mask and spills
         asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(omask));
         if (plane_ok(k + 1)) put_plane(k + 1);
-        if constexpr (PROLONG) {
-          // the coarse plane fine plane k+2 (put next step) needs, and the one after it
-          if (chi < ctop(k + 2)) {
-            ++chi;
-            cput(chi);
-          }
-          if (chi < ctop(k + 3)) cload(chi + 1);
-        }
         load_plane(k + 2);
         __syncthreads();
 #pragma unroll
@@ -1055,7 +735,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
 #pragma unroll
           for (int e = 0; e < OPT; ++e)
             if (oglb[e] >= 0)
-              buf_store<T, MAD_ST_AUX>(*reinterpret_cast<const T*>(P + olds[e]), ro, (uint32_t)oglb[e]);
+              buf_store<T>(*reinterpret_cast<const T*>(P + olds[e]), ro, (uint32_t)oglb[e]);
           if (signals && mo == GHOST - 1) {
             // the edge planes 0..GHOST-1 of this tile are stored: release them, count in
             __threadfence();
@@ -1066,480 +746,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
         }
       }
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// g recomputed in-kernel (declared here, defined with build_g_k below)
-template <typename T>
-__device__ __forceinline__ T gdelta(T fm2, T fm1, T f0, T fp1, T fp2, bool lo, bool hi);
-template <typename T, int DIM, int KIND>
-__device__ __forceinline__ void g_combine(T dxax, T dyay, T dzaz, T dxexy, T dyexy, T dxexz,
-                                          T dzexz, T dyeyz, T dzeyz, T& gx, T& gy, T& gz);
-
-// Fused 4-colour GS sweep of the full 3D operator with g recomputed in-kernel.
-// Reads 24-B tensor records [a_x a_y a_z e_xy e_xz e_yz] (LevelData::ct: cidx point order,
-// GHOST planes like the coefficient records), the dense b and u; writes u out of place.
-// Per voxel-sweep that is the 36 algorithmic bytes (+ the tile halo, mostly L2 hits:
-// neighbouring tiles of one XCD run the same planes together) instead of the 40-48 B of
-// gs_fused3_k, whose records also carry g.  Bit-identical to gs_fused3_k and to per-colour
-// passes on records whose g is build_g_k's (same gdelta / g_combine on the same values).
-//
-// Schedule as gs_fused3_k: z-marching wavefront (step k: stage c updates colour c on plane
-// k-c), overlapped tiles with halo H = 4, a 6-plane LDS ring of u with the x/y mirror images
-// of the domain faces.  Mapping: one thread per 2x2 point block of the tile region
-// (RX x RY = (TX+8) x (TY+8)).  A block holds one point of every colour on every plane, so
-// every stage updates one point per thread, and the block's four records of a plane are
-// read together as a plane stream.  g of plane k needs the tensor of planes k-1..k+1: the
-// z-differences come from the thread's own columns (registers; plane k+1 is loaded one
-// step ahead), the x/y differences from an LDS exchange plane of the in-plane components
-// (a_x a_y e_xy e_xz e_yz of plane k; a block's own neighbours come from registers).  A
-// point's record (tensor, b, g) then waits in registers until its colour's stage, 0..3
-// steps later (at most 2.5 planes of records per block): registers, not LDS, bound the
-// tile.  Domain faces: the reference's one-sided differences (gdelta) from the exchange
-// plane (x/y) and from a reload of plane k-2 (top z face).
-template <int TX, int TY>
-struct FusedGGeom {
-  static constexpr int H = 4;
-  static constexpr int RX = TX + 2 * H, RY = TY + 2 * H;
-  static constexpr int BX = RX / 2, BY = RY / 2, NB = BX * BY;
-  static constexpr int HALF = BX;  // row: even-x half (BX points), then the odd-x half
-  // 2 * PITCH == BX (mod 32): the lanes of a wave (blocks in row-major order) address
-  // consecutive element slots modulo 32 -> conflict-free 4-B and 8-B LDS accesses
-  static constexpr int pitch() {
-    int p = 2 * HALF;
-    while ((2 * p - BX) % 32 != 0) ++p;
-    return p;
-  }
-  static constexpr int PITCH = pitch();
-  static constexpr int PLANE = RY * PITCH;
-  static constexpr int NP = 8;                      // u ring planes (6 in use; 8: slot = m & 7)
-  static constexpr int NXC = 5;                     // exchange components
-  static constexpr int XPLANE = (RY + 2) * PITCH;   // one component, rows -1 .. RY
-  static constexpr int ELEMS = NP * PLANE + NXC * XPLANE;
-};
-
-template <typename T, int TX, int TY, int NT, int MINW = NT / 256>
-__global__ void __launch_bounds__(NT, MINW) gs_fusedg_k(const T* __restrict__ uin, T* __restrict__ uout,
-                                                           const T* __restrict__ b, const T* __restrict__ ct,
-                                                           Geo g, int zc, int ntx, int nty, int zbase,
-                                                           int zstride, int flip_last,
-                                                           uint32_t* __restrict__ sig) {
-  constexpr int NC = 4;
-  using FG = FusedGGeom<TX, TY>;
-  constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, BX = FG::BX, NB = FG::NB;
-  constexpr int HALF = FG::HALF, PITCH = FG::PITCH, PLANE = FG::PLANE, NP = FG::NP;
-  constexpr int XPLANE = FG::XPLANE;
-  constexpr int RS = 6;  // tensor record
-  constexpr uint32_t TS = sizeof(T);
-  static_assert(TX % 4 == 0 && TY % 2 == 0, "2x2 blocks, even BX");
-  static_assert(NB <= NT, "one 2x2 block per thread");
-  extern __shared__ __align__(16) unsigned char fused_smem[];
-  T* const ring = reinterpret_cast<T*>(fused_smem);
-  T* const xb = ring + NP * PLANE + PITCH;  // exchange component c at c * XPLANE, rows -1 .. RY
-
-  int bid = blockIdx.x;
-  {
-    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = bid & 7, idx = bid >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int tiles = ntx * nty;
-  const int chunk = bid / tiles;
-  const int tile = bid - chunk * tiles;
-  const int tyi = tile / ntx;
-  const int txi = tile - tyi * ntx;
-  const int rx0 = txi * TX - H;
-  const int ry0 = tyi * TY - H;
-  const int tid = threadIdx.x;
-  const bool has = tid < NB;
-  const int bx = has ? tid % BX : 0, by = has ? tid / BX : 0;
-  const int nx = g.nx, ny = g.ny, sy = (int)g.sy, hx0 = g.hx0;
-  const bool interior = rx0 >= 2 && rx0 + RX <= nx - 2 && ry0 >= 2 && ry0 + RY <= ny - 2;
-
-  const int p0 = zbase + chunk * zstride;
-  const int p1 = min(p0 + zc, g.nz);
-  const bool flip = flip_last != 0 && chunk == (int)(gridDim.x / tiles) - 1;
-  int64_t sz = g.sz;
-  int zlo_g = g.zlo_ghost, zhi_g = g.zhi_ghost, zpar = g.zoff;
-  int z0 = p0, z1 = p1;
-  if (flip) {
-    const int64_t top = (int64_t)(g.nz - 1) * g.sz;
-    uin += top;
-    uout += top;
-    b += top;
-    ct += top * RS;
-    sz = -g.sz;
-    zlo_g = g.zhi_ghost;
-    zhi_g = g.zlo_ghost;
-    zpar = g.zoff + g.nz - 1;
-    z0 = g.nz - p1;
-    z1 = g.nz - p0;
-  }
-  const int zlo = zlo_g ? -GHOST : 0;
-  const int zhi = zhi_g ? g.nz + GHOST : g.nz;
-  const int ulo = zlo_g ? -(GHOST - 1) : 0;
-  const int uhi = zhi_g ? g.nz + GHOST - 1 : g.nz;
-  const bool signals = sig != nullptr && z0 == 0 && zlo_g;
-  // first step with (k + zpar) even, so step k0 + u has plane parity u & 1
-  const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + zpar) & 1);
-  const int kend = z1 + NC - 2;
-
-  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
-
-  // per point s = ox + 2 oy of the block: u / b source and tensor-record byte offsets in
-  // a plane (mirrored outside the domain: in bounds, values unused), LDS element offset in
-  // a plane slot, face flags for the one-sided g differences, output offset
-  // (LDS offsets are one per thread plus a compile-time term per point; an output point
-  // lies in the domain, so its store offset is its unmirrored source offset)
-  uint32_t usrc[4], tof[4];
-  const int uo0 = 2 * by * PITCH + bx;
-  auto uofs = [&](int s) { return uo0 + (s >> 1) * PITCH + (s & 1) * HALF; };
-  uint32_t bflags = 0;  // 4 bits per point: x low, x high, y low, y high face
-  uint32_t omask = 0;   // bit s: point s is a tile-interior output point
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int ox = s & 1, oy = s >> 1;
-    const int li = 2 * bx + ox, lj = 2 * by + oy;
-    const int gi = rx0 + li, gj = ry0 + lj;
-    const int gim = interior ? gi : mirror(gi, nx), gjm = interior ? gj : mirror(gj, ny);
-    usrc[s] = (uint32_t)(gjm * sy + gim) * TS;
-    tof[s] = (uint32_t)(gjm * sy + (gim & 1) * hx0 + (gim >> 1)) * (TS * RS);
-    const bool dom = gi >= 0 && gi < nx && gj >= 0 && gj < ny;
-    if (dom && has)
-      bflags |= ((gi == 0 ? 1u : 0u) | (gi == nx - 1 ? 2u : 0u) | (gj == 0 ? 4u : 0u) |
-                 (gj == ny - 1 ? 8u : 0u)) << (4 * s);
-    const bool out = has && li >= H && li < H + TX && lj >= H && lj < H + TY && gi < nx && gj < ny;
-    omask |= (out ? 1u : 0u) << s;
-  }
-  // stage c at plane parity PM updates point s(c, PM) of the block; valid and ghost-image
-  // bits as in gs_fused3_k
-  uint32_t vmask = 0, gmask = 0;
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int PM = 0; PM < 2; ++PM) {
-      const int ox = (c & 1) ^ PM, oy = ((c >> 1) & 1) ^ PM;
-      const int li = 2 * bx + ox, lj = 2 * by + oy;
-      const int gi = rx0 + li, gj = ry0 + lj;
-      const bool ok = has && li >= c + 1 && li < RX - c - 1 && lj >= c + 1 && lj < RY - c - 1 &&
-                      gi >= 0 && gi < nx && gj >= 0 && gj < ny;
-      vmask |= (ok ? 1u : 0u) << (c * 2 + PM);
-      const uint32_t gb = (ok && gi == 1 ? 1u : 0u) | (ok && gi == nx - 2 ? 2u : 0u) |
-                          (ok && gj == 1 ? 4u : 0u) | (ok && gj == ny - 2 ? 8u : 0u);
-      gmask |= gb << (4 * (c * 2 + PM));
-    }
-
-  auto slot = [](int m) { return m & (NP - 1); };
-  auto plane_ok = [&](int m) { return m >= zlo && m < zhi; };
-  auto stage_on = [&](int c, int m) {
-    const int h = NC - 1 - c;
-    return m >= z0 - h && m < z1 + h && m >= ulo && m < uhi;
-  };
-
-  struct PRec {
-    Coefs<T> q;
-    T b;
-  };
-
-  // the body, with the z-reflection (the last chunk of a single-launch rank-slab sweep) a
-  // compile-time property: no per-difference selects in the common case
-  auto run = [&](auto flip_c) {
-    constexpr bool FLIP = decltype(flip_c)::value;
-    T up[4];
-    T tn[4][4][RS];  // tensor of plane k, buffer (k - kbeg) & 3, per point
-    T bn[4][4];      // b of that plane
-    PRec rec[4][4];  // records waiting for their stage, buffer (plane - kbeg) & 3
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        rec[q][s].q = Coefs<T>{};
-        rec[q][s].b = T(0);
-      }
-
-    auto load_u = [&](int m) {
-      m = min(max(m, zlo), zhi - 1);
-      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) up[s] = buf_load<T>(rs, usrc[s], 0u);
-    };
-    auto put_u = [&](int m) {
-      T* P = ring + slot(m) * PLANE;
-      if (has) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) P[uofs(s)] = up[s];
-      }
-    };
-    auto load_t = [&](int m, T (&t)[4][RS], T (&bb)[4]) {
-#ifdef MAD_PG_NO_T  // measurement builds only: no tensor / b stream
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int q = 0; q < RS; ++q) t[s][q] = T(0.01 * (q + 1) + 0.001 * m);
-        bb[s] = T(0.5);
-      }
-      return;
-#endif
-      m = min(max(m, zlo), zhi - 1);
-      const __amdgpu_buffer_rsrc_t rt = buf_rsrc(ct + (int64_t)m * sz * RS);
-      const __amdgpu_buffer_rsrc_t rb = buf_rsrc(b + (int64_t)m * sz);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        buf_load_rec<T, RS>(rt, tof[s], t[s]);
-        bb[s] = buf_load<T>(rb, usrc[s], 0u);
-      }
-    };
-    // exchange plane <- a_x a_y e_xy e_xz e_yz of this thread's four points
-    auto put_x = [&](const T (&t)[4][RS]) {
-      if (has) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          T* P = xb + uofs(s);
-          P[0 * XPLANE] = t[s][0];
-          P[1 * XPLANE] = t[s][1];
-          P[2 * XPLANE] = t[s][3];
-          P[3 * XPLANE] = t[s][4];
-          P[4 * XPLANE] = t[s][5];
-        }
-      }
-    };
-    // records of plane k: g from the exchange plane (x/y) and the z neighbours' tensors
-    auto make_rec = [&](int k, const T (&tc)[4][RS], const T (&bc)[4], const T (&tm)[4][RS],
-                        const T (&tp)[4][RS], PRec (&out)[4]) {
-#pragma clang fp contract(off)
-      // fast path: central differences in x/y (the block's own neighbours from registers,
-      // the others from the exchange plane) and z (physical +z minus -z), g per point
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int ox = s & 1, oy = s >> 1;
-        const T* X = xb + uofs(s);
-#ifndef MAD_PG_NO_X
-        auto xp = [&](int C, int XC) { return ox == 0 ? tc[s + 1][C] : X[XC * XPLANE + 1 - HALF]; };
-        auto xm = [&](int C, int XC) { return ox == 1 ? tc[s - 1][C] : X[XC * XPLANE + HALF - 1]; };
-        auto yp = [&](int C, int XC) { return oy == 0 ? tc[s + 2][C] : X[XC * XPLANE + PITCH]; };
-        auto ym = [&](int C, int XC) { return oy == 1 ? tc[s - 2][C] : X[XC * XPLANE - PITCH]; };
-#else  // measurement builds only: in-plane differences from registers only
-        (void)X;
-        (void)ox;
-        (void)oy;
-        auto xp = [&](int C, int) { return tc[s ^ 1][C]; };
-        auto xm = [&](int C, int) { return tc[s][C]; };
-        auto yp = [&](int C, int) { return tc[s ^ 2][C]; };
-        auto ym = [&](int C, int) { return tc[s][C]; };
-#endif
-        const T dxax = xp(0, 0) - xm(0, 0);
-        const T dyay = yp(1, 1) - ym(1, 1);
-        const T dxexy = xp(3, 2) - xm(3, 2);
-        const T dyexy = yp(3, 2) - ym(3, 2);
-        const T dxexz = xp(4, 3) - xm(4, 3);
-        const T dyeyz = yp(5, 4) - ym(5, 4);
-        const T dzaz = FLIP ? tm[s][2] - tp[s][2] : tp[s][2] - tm[s][2];
-        const T dzexz = FLIP ? tm[s][4] - tp[s][4] : tp[s][4] - tm[s][4];
-        const T dzeyz = FLIP ? tm[s][5] - tp[s][5] : tp[s][5] - tm[s][5];
-        PRec& R = out[s];
-        R.q.ax = tc[s][0];
-        R.q.ay = tc[s][1];
-        R.q.az = tc[s][2];
-        R.q.exy = tc[s][3];
-        R.q.exz = tc[s][4];
-        R.q.eyz = tc[s][5];
-        g_combine<T, 3, KFULL>(dxax, dyay, dzaz, dxexy, dyexy, dxexz, dzexz, dyeyz, dzeyz, R.q.gx,
-                               R.q.gy, R.q.gz);
-        R.b = bc[s];
-      }
-      // domain faces (x/y: tiles touching a face; z: two planes per sweep): g of the
-      // flagged points again, with the reference's one-sided second-order differences
-      // (x/y: rows / half-rows +-2 away in the exchange plane; z: the planes two away,
-      // reloaded -- their buffers are gone or not yet filled)
-      const bool lb = k == 0 && !zlo_g, hb = k == g.nz - 1 && !zhi_g;
-#ifdef MAD_PG_NO_FACE  // measurement builds only: no face corrections (wrong at faces)
-      if (false) {
-#else
-      if (bflags != 0u || lb || hb) {
-#endif
-        const bool zlo_f = FLIP ? hb : lb, zhi_f = FLIP ? lb : hb;  // physical z faces
-        const __amdgpu_buffer_rsrc_t rm = buf_rsrc(ct + (int64_t)max(k - 2, zlo) * sz * RS);
-        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(ct + (int64_t)min(k + 2, zhi - 1) * sz * RS);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const uint32_t bf = (bflags >> (4 * s)) & 15u;
-          if (!bf && !lb && !hb) continue;
-          const int ox = s & 1, oy = s >> 1;
-          const T* X = xb + uofs(s);
-          const bool xl = bf & 1u, xh = bf & 2u, yl = bf & 4u, yh = bf & 8u;
-          auto xp = [&](int C, int XC) { return ox == 0 ? tc[s + 1][C] : X[XC * XPLANE + 1 - HALF]; };
-          auto xm = [&](int C, int XC) { return ox == 1 ? tc[s - 1][C] : X[XC * XPLANE + HALF - 1]; };
-          auto yp = [&](int C, int XC) { return oy == 0 ? tc[s + 2][C] : X[XC * XPLANE + PITCH]; };
-          auto ym = [&](int C, int XC) { return oy == 1 ? tc[s - 2][C] : X[XC * XPLANE - PITCH]; };
-          auto dx = [&](int C, int XC) {
-            return gdelta(X[XC * XPLANE - 1], xm(C, XC), tc[s][C], xp(C, XC), X[XC * XPLANE + 1], xl, xh);
-          };
-          auto dy = [&](int C, int XC) {
-            return gdelta(X[XC * XPLANE - 2 * PITCH], ym(C, XC), tc[s][C], yp(C, XC),
-                          X[XC * XPLANE + 2 * PITCH], yl, yh);
-          };
-          auto dz = [&](int C) {
-            T lm2 = T(0), lp2 = T(0);
-            if (lb || hb) {
-              lm2 = buf_load<T>(rm, tof[s], C * TS);
-              lp2 = buf_load<T>(rp, tof[s], C * TS);
-            }
-            const T lm1 = tm[s][C], lp1 = tp[s][C];
-            // logical k-2, k-1, k+1, k+2 -> physical -2, -1, +1, +2
-            return FLIP ? gdelta(lp2, lp1, tc[s][C], lm1, lm2, zlo_f, zhi_f)
-                        : gdelta(lm2, lm1, tc[s][C], lp1, lp2, zlo_f, zhi_f);
-          };
-          PRec& R = out[s];
-          g_combine<T, 3, KFULL>(dx(0, 0), dy(1, 1), dz(2), dx(3, 2), dy(3, 2), dx(4, 3), dz(4), dy(5, 4),
-                                 dz(5), R.q.gx, R.q.gy, R.q.gz);
-        }
-      }
-    };
-    auto stage = [&](int c, int k, int PM, const PRec (&rq)[4]) {
-      const int m = k - c;
-      if (!stage_on(c, m)) return;
-#ifdef MAD_PG_NO_STAGE  // measurement builds only: no stage reads / arithmetic
-      if (c >= 0) {
-        const int s0 = ((c & 1) ^ PM) + 2 * (((c >> 1) & 1) ^ PM);
-        if ((vmask >> (c * 2 + PM)) & 1u) ring[slot(m) * PLANE + uofs(s0)] = rq[s0].q.gx + rq[s0].b;
-        return;
-      }
-#endif
-      const int ox = (c & 1) ^ PM, oy = ((c >> 1) & 1) ^ PM, s = ox + 2 * oy;
-      const int zm = (m == 0 && !zlo_g) ? 1 : m - 1;
-      const int zp = (m == g.nz - 1 && !zhi_g) ? g.nz - 2 : m + 1;
-      T* A0 = ring + slot(m) * PLANE + uofs(s);
-      // physical -z / +z neighbour planes (swapped in the reflected view)
-      const T* Am = ring + slot(FLIP ? zp : zm) * PLANE + uofs(s);
-      const T* Ap = ring + slot(FLIP ? zm : zp) * PLANE + uofs(s);
-      const int ox_p = ox ? 1 - HALF : HALF;
-      const int ox_m = ox ? -HALF : HALF - 1;
-      T nb[18];
-      nb[0] = A0[ox_p];
-      nb[1] = A0[ox_m];
-      nb[2] = A0[PITCH];
-      nb[3] = A0[-PITCH];
-      nb[4] = Ap[0];
-      nb[5] = Am[0];
-      nb[6] = A0[ox_p + PITCH];
-      nb[7] = A0[ox_p - PITCH];
-      nb[8] = A0[ox_m + PITCH];
-      nb[9] = A0[ox_m - PITCH];
-      nb[10] = Ap[ox_p];
-      nb[11] = Am[ox_p];
-      nb[12] = Ap[ox_m];
-      nb[13] = Am[ox_m];
-      nb[14] = Ap[PITCH];
-      nb[15] = Am[PITCH];
-      nb[16] = Ap[-PITCH];
-      nb[17] = Am[-PITCH];
-      T D, S;
-      stencil_combine<T, 3, KFULL>(rq[s].q, nb, D, S);
-      const T v = gs_update(rq[s].b, S, D);
-      const int bit = c * 2 + PM;
-      if ((vmask >> bit) & 1u) *A0 = v;
-#ifdef MAD_PG_NO_FACE
-      if (false) {
-#else
-      if (!interior) {
-#endif
-        const uint32_t gb = (gmask >> (4 * bit)) & 15u;
-        if (gb) {
-          // mirror images u~(-1) = u(1), u~(n) = u(n-2): same row parity, +-1 in the half
-          // row (x) and +-2 rows (y); corners need both (gb is 0 for invalid points)
-          const int xs[3] = {0, (gb & 1u) ? -1 : 0, (gb & 2u) ? 1 : 0};
-          const int ys[3] = {0, (gb & 4u) ? -2 * PITCH : 0, (gb & 8u) ? 2 * PITCH : 0};
-#pragma unroll
-          for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int bq = 0; bq < 3; ++bq) {
-              if ((a == 0 && bq == 0) || (a > 0 && xs[a] == 0) || (bq > 0 && ys[bq] == 0)) continue;
-              A0[xs[a] + ys[bq]] = v;
-            }
-        }
-      }
-    };
-
-    // prologue: u planes kbeg-1, kbeg in the ring, kbeg+1 in registers; tensors of planes
-    // kbeg-1 .. kbeg+1 in buffers 3, 0, 1
-    for (int m = kbeg - 1; m <= kbeg; ++m)
-      if (plane_ok(m)) {
-        load_u(m);
-        put_u(m);
-      }
-    load_u(kbeg + 1);
-    load_t(kbeg - 1, tn[3], bn[3]);
-    load_t(kbeg, tn[0], bn[0]);
-    load_t(kbeg + 1, tn[1], bn[1]);
-
-    // Whole groups of 4 steps: a step past kend runs no stage and stores nothing (stage_on,
-    // the output range), and an unconditional body keeps the records' live ranges to their
-    // real uses (a guarded step would keep every pending record alive across its join).
-    // Barriers: one after the plane / exchange writes, one after each of stages 0-2.  None
-    // after stage 3: the next step writes ring slot k+3 (8 slots, nobody reads it) and the
-    // exchange plane (last read before stage 0), and a thread's stores read only its own
-    // points.
-    for (int k0 = kbeg; k0 <= kend; k0 += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u;
-        asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(bflags), "+v"(omask));
-        if (plane_ok(k + 1)) put_u(k + 1);
-        put_x(tn[u]);
-        load_u(k + 2);
-        __syncthreads();
-        make_rec(k, tn[u], bn[u], tn[(u + 3) & 3], tn[(u + 1) & 3], rec[u]);
-        // plane k+2's tensor: issued once g of plane k is formed (plane k's tensor now
-        // lives on in the records), in flight through this step's stages
-        load_t(k + 2, tn[(u + 2) & 3], bn[(u + 2) & 3]);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          stage(c, k, (u ^ c) & 1, rec[(u - c) & 3]);
-          if (c < NC - 1) __syncthreads();
-        }
-        const int mo = k - NC + 1;
-        if (mo >= z0 && mo < z1) {
-          const T* P = ring + slot(mo) * PLANE;
-          const __amdgpu_buffer_rsrc_t ro = buf_rsrc(uout + (int64_t)mo * sz);
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-#ifndef MAD_PG_NO_STORE  // measurement builds only: no output stores
-            if ((omask >> s) & 1u) buf_store<T>(P[uofs(s)], ro, usrc[s]);
-#else
-            if ((omask >> s) & 1u && P[uofs(s)] == T(-12345.678)) buf_store<T>(P[uofs(s)], ro, usrc[s]);
-#endif
-          if (signals && mo == GHOST - 1) {
-            __threadfence();
-            __syncthreads();
-            if (tid == 0)
-              __hip_atomic_fetch_add(sig + (FLIP ? 1 : 0), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-        }
-      }
-    }
-  };
-  if (flip)
-    run(std::true_type{});
-  else
-    run(std::false_type{});
-}
-
-// tensor records (a_x a_y a_z e_xy e_xz e_yz) of the full 3D operator from its coefficient
-// records (fields 0-2 and 6-8), plane range [p0, p1) (ghost planes included)
-template <typename T>
-__global__ void __launch_bounds__(256) pack_tensor_k(const T* __restrict__ cf, T* __restrict__ ct,
-                                                     int64_t sz, int rs, int p0, int64_t n) {
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p = (int64_t)p0 * sz + q;
-    const T* s = cf + p * rs;
-    T* d = ct + p * 6;
-    d[0] = s[0];
-    d[1] = s[1];
-    d[2] = s[2];
-    d[3] = s[6];
-    d[4] = s[7];
-    d[5] = s[8];
   }
 }
 
@@ -2257,268 +1463,6 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
         }
         ++K;
         if (K < K1) ztaps(K);
-      }
-    }
-  }
-}
-
-// resid_restrict3g_k: resid_restrict3_k for the full 3D operator with g recomputed from
-// the 24-B tensor records (ct, pack_tensor_k) instead of read from the 36-B coefficient
-// records -- 24 + 4 (b) + 4 (u) bytes per fine voxel instead of 44.  The u region (the
-// residual tile + 1) is the unit of every load: per fine plane each thread loads its
-// region points' six tensor components; the in-plane ones (a_x a_y e_xy e_xz e_yz) go to
-// a two-slot LDS plane pair for the x / y differences, the z ones (a_z e_xz e_yz) into a
-// per-thread register window of planes f-1 .. f+1 for the z differences (the faces'
-// second planes f+2 / f-2 are loaded where they are needed).  g is gdelta / g_combine of the same values
-// build_g_k reads (neighbour planes clamped as there), so b_c is bit-identical to
-// resid_restrict3_k's.  u: a 3-slot LDS ring.  With zx set, the coarse x is zeroed on the
-// way (the descent's fill, MAD.hxx:415-416).  One rank, nx, ny >= 16, nz >= 2.
-template <typename T, int CX, int CY, int NT, int MINW = 1>
-__global__ void __launch_bounds__(NT, MINW) resid_restrict3g_k(
-    const T* __restrict__ u, const T* __restrict__ b, const T* __restrict__ ct, Geo gf,
-    T* __restrict__ coarse, T* __restrict__ zx, Geo gc, int cx, int cy, int cz, int kc, int ntx) {
-  static_assert(CX * CY <= NT, "one coarse point per thread");
-  constexpr int FX = 2 * CX + 2, FY = 2 * CY + 2, FP = FX * FY;  // residual tile
-  constexpr int UX = FX + 2, UY = FY + 2, UP = UX * UY;          // region (tile + 1)
-  constexpr int EPT = (UP + NT - 1) / NT;
-  constexpr uint32_t TS = sizeof(T);
-  __shared__ T ring[3 * UP];
-  __shared__ T tpl[2 * 5 * UP];
-  __shared__ T rt[FP];
-  const int tiles = ntx * ((gc.ny + CY - 1) / CY);
-  const int chunk = blockIdx.x / tiles;
-  const int t = blockIdx.x - chunk * tiles;
-  const int tyi = t / ntx, txi = t - (t / ntx) * ntx;
-  const int I0 = txi * CX, J0 = tyi * CY;
-  const int tid = threadIdx.x;
-  const int nx = gf.nx, ny = gf.ny, nz = gf.nz, sy = (int)gf.sy, hx0 = gf.hx0;
-  const int64_t sz = gf.sz;
-  const int fx0 = 2 * I0 - 1, fy0 = 2 * J0 - 1;
-  const int ux0 = fx0 - 1, uy0 = fy0 - 1;
-  auto mirror = [](int v, int n) { return v < 0 ? min(-v, n - 1) : (v >= n ? max(2 * (n - 1) - v, 0) : v); };
-  const bool cthr = tid < CX * CY;
-  const int I = I0 + tid % CX, J = J0 + (tid / CX) % CY;
-  const bool ok = cthr && I < gc.nx && J < gc.ny;
-  // region points of this thread: mirrored sources (u dense, tensor record; a residual
-  // point lies in the domain, so its rhs offset is its u source offset) and rf = residual-
-  // tile index + 1 (0: not a residual point -- outside the tile or the domain, never
-  // tapped) << 4 | face flags (x lo / hi, y lo / hi as build_g_k sets them)
-  uint32_t u_src[EPT], t_src[EPT], rf[EPT];
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const int q = tid + e * NT;
-    const int qq = min(q, UP - 1);
-    const int lj = qq / UX, li = qq - (qq / UX) * UX;
-    const int xf = ux0 + li, yf = uy0 + lj;
-    const int xs = mirror(xf, nx), ys = mirror(yf, ny);
-    u_src[e] = (uint32_t)(ys * sy + xs) * TS;
-    t_src[e] = (uint32_t)(ys * sy + (xs & 1) * hx0 + (xs >> 1)) * (TS * 6);
-    const bool res = q < UP && li >= 1 && li <= FX && lj >= 1 && lj <= FY && xf >= 0 && xf < nx &&
-                     yf >= 0 && yf < ny;
-    const bool xl = xf == 0, xh = !xl && xf == nx - 1, yl = yf == 0, yh = !yl && yf == ny - 1;
-    rf[e] = (res ? (uint32_t)((lj - 1) * FX + li) << 4 : 0u) | (xl ? 1u : 0u) | (xh ? 2u : 0u) |
-            (yl ? 4u : 0u) | (yh ? 8u : 0u);
-  }
-  const int K0 = chunk * kc, K1 = min(K0 + kc, gc.nz);
-  int iz[4];
-  T wz[4];
-  rtaps4<T>(K0, gc.nz, cz, iz, wz);
-  const int f_lo = iz[0];
-  rtaps4<T>(K1 - 1, gc.nz, cz, iz, wz);
-  const int f_hi = max(max(iz[0], iz[1]), max(iz[2], iz[3]));
-
-  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
-  auto wave_in = [&](int e) { return wbase + e * NT < UP; };
-  T up[EPT];
-  T P[EPT][6];     // tensor record of the plane in flight
-  T W[EPT][3][3];  // a_z e_xz e_yz of planes f-1 .. f+1 (after the push of f+1)
-  T bv[EPT];
-  auto uslot = [](int m) { return ring + ((unsigned)m % 3u) * UP; };
-  auto load_plane = [&](int m) {
-    m = min(max(m, 0), nz - 1);
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
-#pragma unroll
-    for (int e = 0; e < EPT; ++e)
-      if (e == 0 || wave_in(e)) up[e] = buf_load<T>(rs, u_src[e], 0u);
-  };
-  auto put_plane = [&](int m) {
-    T* S = uslot(m);
-#pragma unroll
-    for (int e = 0; e < EPT; ++e)
-      if (tid + e * NT < UP) S[tid + e * NT] = up[e];
-  };
-  auto load_t = [&](int m) {
-    m = min(max(m, 0), nz - 1);
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(ct + (int64_t)m * sz * 6);
-#pragma unroll
-    for (int e = 0; e < EPT; ++e)
-      if (e == 0 || wave_in(e)) buf_load_rec<T, 6>(rs, t_src[e], P[e]);
-  };
-  // plane m (in P) -> LDS slot m & 1 and the z window
-  auto push = [&](int m) {
-    T* S = tpl + (m & 1) * 5 * UP;
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      const int q = tid + e * NT;
-      if (q < UP) {
-        S[q] = P[e][0];
-        S[UP + q] = P[e][1];
-        S[2 * UP + q] = P[e][3];
-        S[3 * UP + q] = P[e][4];
-        S[4 * UP + q] = P[e][5];
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) W[e][s][c] = W[e][s + 1][c];
-      W[e][2][0] = P[e][2];
-      W[e][2][1] = P[e][4];
-      W[e][2][2] = P[e][5];
-    }
-  };
-  auto load_b = [&](int m) {
-    const __amdgpu_buffer_rsrc_t rb = buf_rsrc(b + (int64_t)m * sz);
-#pragma unroll
-    for (int e = 0; e < EPT; ++e)
-      if (e == 0 || wave_in(e)) bv[e] = buf_load<T>(rb, u_src[e], 0u);
-  };
-
-#pragma unroll
-  for (int e = 0; e < EPT; ++e)
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) W[e][s][c] = T(0);
-  if (f_lo - 1 >= 0) {
-    load_plane(f_lo - 1);
-    put_plane(f_lo - 1);
-  }
-  load_plane(f_lo);
-  put_plane(f_lo);
-  load_plane(f_lo + 1);
-  load_t(f_lo - 1);
-  push(f_lo - 1);
-  load_t(f_lo);
-  push(f_lo);
-  load_t(f_lo + 1);  // pushed at the first step's top
-  load_b(f_lo);
-  T win[4];
-  int K = K0;
-  rtaps4<T>(K, gc.nz, cz, iz, wz);
-  for (int f = f_lo; f <= f_hi; ++f) {
-    if (f + 1 < nz) put_plane(f + 1);
-    push(f + 1);  // window: planes f-1 .. f+1
-    load_plane(f + 2);
-    __syncthreads();  // u planes f-1..f+1 and tensor plane f staged; last restriction done
-    const int zm = f == 0 ? f + 1 : f - 1;
-    const int zp = f == nz - 1 ? f - 1 : f + 1;
-    const bool zl = f == 0, zh = !zl && f == nz - 1;
-    const T* TP = tpl + (f & 1) * 5 * UP;
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      if (e > 0 && !wave_in(e)) continue;
-      const uint32_t fe = rf[e];
-      if (fe < 16u) continue;
-      const int q = tid + e * NT;
-      const T* A = TP + q;
-      T dxax, dyay, dxexy, dyexy, dxexz, dyeyz;
-      if (fe & 15u) {  // x / y face point: the one-sided points (inside the region there)
-        const bool xl = fe & 1u, xh = fe & 2u, yl = fe & 4u, yh = fe & 8u;
-        const int xm2 = xh ? -2 : 0, xp2 = xl ? 2 : 0, ym2 = yh ? -2 * UX : 0, yp2 = yl ? 2 * UX : 0;
-        dxax = gdelta(A[xm2], A[-1], A[0], A[1], A[xp2], xl, xh);
-        dyay = gdelta(A[UP + ym2], A[UP - UX], A[UP], A[UP + UX], A[UP + yp2], yl, yh);
-        dxexy = gdelta(A[2 * UP + xm2], A[2 * UP - 1], A[2 * UP], A[2 * UP + 1], A[2 * UP + xp2], xl, xh);
-        dyexy = gdelta(A[2 * UP + ym2], A[2 * UP - UX], A[2 * UP], A[2 * UP + UX], A[2 * UP + yp2], yl, yh);
-        dxexz = gdelta(A[3 * UP + xm2], A[3 * UP - 1], A[3 * UP], A[3 * UP + 1], A[3 * UP + xp2], xl, xh);
-        dyeyz = gdelta(A[4 * UP + ym2], A[4 * UP - UX], A[4 * UP], A[4 * UP + UX], A[4 * UP + yp2], yl, yh);
-      } else {  // interior: central differences (gdelta's own interior branch)
-        dxax = gdelta(T(0), A[-1], T(0), A[1], T(0), false, false);
-        dyay = gdelta(T(0), A[UP - UX], T(0), A[UP + UX], T(0), false, false);
-        dxexy = gdelta(T(0), A[2 * UP - 1], T(0), A[2 * UP + 1], T(0), false, false);
-        dyexy = gdelta(T(0), A[2 * UP - UX], T(0), A[2 * UP + UX], T(0), false, false);
-        dxexz = gdelta(T(0), A[3 * UP - 1], T(0), A[3 * UP + 1], T(0), false, false);
-        dyeyz = gdelta(T(0), A[4 * UP - UX], T(0), A[4 * UP + UX], T(0), false, false);
-      }
-      // the faces' second planes f+2 / f-2 are loaded here (uniform: two planes only)
-      T z2[3] = {T(0), T(0), T(0)};
-      if (zl || zh) {
-        T r2[6];
-        buf_load_rec<T, 6>(buf_rsrc(ct + (int64_t)min(max(zl ? f + 2 : f - 2, 0), nz - 1) * sz * 6),
-                           t_src[e], r2);
-        z2[0] = r2[2];
-        z2[1] = r2[4];
-        z2[2] = r2[5];
-      }
-      const T dzaz = gdelta(z2[0], W[e][0][0], W[e][1][0], W[e][2][0], z2[0], zl, zh);
-      const T dzexz = gdelta(z2[1], W[e][0][1], W[e][1][1], W[e][2][1], z2[1], zl, zh);
-      const T dzeyz = gdelta(z2[2], W[e][0][2], W[e][1][2], W[e][2][2], z2[2], zl, zh);
-      Coefs<T> c;
-      g_combine<T, 3, KFULL>(dxax, dyay, dzaz, dxexy, dyexy, dxexz, dzexz, dyeyz, dzeyz, c.gx, c.gy, c.gz);
-      c.ax = A[0];
-      c.ay = A[UP];
-      c.az = W[e][1][0];
-      c.exy = A[2 * UP];
-      c.exz = A[3 * UP];
-      c.eyz = A[4 * UP];
-      const T* P0 = uslot(f) + q;
-      const T* Pm = uslot(zm) + q;
-      const T* Pp = uslot(zp) + q;
-      T nb[18];
-      nb[0] = P0[1];
-      nb[1] = P0[-1];
-      nb[2] = P0[UX];
-      nb[3] = P0[-UX];
-      nb[4] = Pp[0];
-      nb[5] = Pm[0];
-      nb[6] = P0[1 + UX];
-      nb[7] = P0[1 - UX];
-      nb[8] = P0[-1 + UX];
-      nb[9] = P0[-1 - UX];
-      nb[10] = Pp[1];
-      nb[11] = Pm[1];
-      nb[12] = Pp[-1];
-      nb[13] = Pm[-1];
-      nb[14] = Pp[UX];
-      nb[15] = Pm[UX];
-      nb[16] = Pp[-UX];
-      nb[17] = Pm[-UX];
-      T D, S;
-      stencil_combine<T, 3, KFULL>(c, nb, D, S);
-      rt[(fe >> 4) - 1] = resid_value(bv[e], D, P0[0], S);
-      __builtin_amdgcn_sched_barrier(0);  // one point at a time: registers are the limit
-    }
-    // next plane's tensor records and rhs: in flight across the restriction (P is dead
-    // during the point computation, which is where the registers peak)
-    load_t(f + 2);
-    if (f < f_hi) load_b(f + 1);
-    __syncthreads();  // residual tile of plane f complete
-    {
-#pragma clang fp contract(off)  // restrict3_k's explicit-fma order
-      int ix[4], iy[4];  // recomputed per plane: registers are the limit here
-      T wx[4], wy[4];
-      rtaps4<T>(min(I, gc.nx - 1), gc.nx, cx, ix, wx);
-      rtaps4<T>(min(J, gc.ny - 1), gc.ny, cy, iy, wy);
-      T vz = T(0);
-#pragma unroll
-      for (int bq = 0; bq < 4; ++bq) {
-        const T* row = rt + (iy[bq] - fy0) * FX - fx0;
-        T vy = T(0);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) vy = fma(wx[a], row[ix[a]], vy);
-        vz = fma(wy[bq], vy, vz);
-      }
-      win[f & 3] = vz;
-      while (K < K1 && max(max(iz[0], iz[1]), max(iz[2], iz[3])) == f) {
-        T v = T(0);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v = fma(wz[c], win[iz[c] & 3], v);
-        if (ok) {
-          const int64_t o = I + gc.sy * J + gc.sz * (int64_t)K;
-          coarse[o] = v;
-          if (zx) zx[o] = T(0);
-        }
-        ++K;
-        if (K < K1) rtaps4<T>(K, gc.nz, cz, iz, wz);
       }
     }
   }

@@ -31,7 +31,6 @@
 #include "../../include/mad.h"
 #include "mad_comm.hpp"
 #include "mad_kernels.hpp"
-#include "mad_tsweep.hpp"
 
 using namespace mad;
 
@@ -265,15 +264,6 @@ struct LevelData {
   T* t = nullptr;  // WJ ping-pong / scratch
   T* cf = nullptr;        // field 0, plane 0 (ghost planes precede it on rank slabs)
   T* cf_alloc = nullptr;
-  // full 3D tensor records [a_x a_y a_z e_xy e_xz e_yz] (same point order and ghost planes
-  // as cf, no g): the fused sweep gs_fusedg_k reads these and recomputes g
-  T* ct = nullptr;
-  T* ct_alloc = nullptr;
-  // tensor array of the g-free level sweep gs_tsweep_k (build_gt_k: natural x order, TSweepGeom::PAD
-  // padding points per side with the domain-face ghosts, GHOST planes); gt = plane 0
-  T* gt = nullptr;
-  T* gt_alloc = nullptr;
-  TGeo tg{};
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -294,15 +284,10 @@ struct LevelData {
   uint32_t* sig = nullptr;
   uint32_t sig_epoch = 0;
 };
-// z-depth of a rank slab's boundary chunks (>= GHOST); MAD_BOUNDARY_PLANES overrides
-// it for tuning runs
-inline int boundary_planes() {
-  static const int v = [] {
-    const char* e = std::getenv("MAD_BOUNDARY_PLANES");
-    return e ? std::max(GHOST, std::atoi(e)) : 8;
-  }();
-  return v;
-}
+// z-depth of a rank slab's boundary chunks (>= GHOST; 4 measured 0.231 vs 0.228 ms per 8-rank
+// sweep, profiles/r02_slab_tiles.log)
+constexpr int BOUNDARY_PLANES = 8;
+inline int boundary_planes() { return BOUNDARY_PLANES; }
 
 template <typename T>
 class Solver final : public SolverBase {
@@ -343,13 +328,10 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipMalloc(&L.alloc[a], sizeof(T) * tot));
         HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
       }
-      // x and t (the fused sweep's ping-pong pair) start xshift elements past the
-      // margin so that a tile region's first column (x = -H) is cache-line aligned
-      const int64_t xs = x_shift();
-      L.x = L.alloc[0] + margin + L.ghost + xs;
+      L.x = L.alloc[0] + margin + L.ghost;
       L.b = L.alloc[1] + margin + L.ghost;
       L.r = L.alloc[2] + margin + L.ghost;
-      L.t = L.alloc[3] + margin + L.ghost + xs;
+      L.t = L.alloc[3] + margin + L.ghost;
       // coefficient records, point-interleaved (mad_kernels.hpp, cidx); 3D levels keep
       // GHOST coefficient planes per side: neighbour planes on rank slabs (the fused
       // sweep recomputes colours on them), padding for masked border lanes otherwise
@@ -359,14 +341,8 @@ class Solver final : public SolverBase {
       // every time step after ~2 cycles (~12 level-0 record passes), where the 2.2 ms
       // scatter of b into the 40-B records (partial-line writes, 512^3) costs more than
       // it saves (VED diffusion 126 -> 116.5 ms without it, profiles/r01_brec_ab.log).
-      // MAD_BREC=0/1 overrides (A/B runs).
-      // The full-tensor GS sweep (gs_fusedg_k) reads the dense b with its plane stream, so
-      // it needs no record b.
-      bool brec_on = c->d.cycle == MAD_SMOOTHER &&
-                     !(c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL &&
-                       (fusedg_wanted(c->d) || tsweep_level(c, l, L)));
+      bool brec_on = c->d.cycle == MAD_SMOOTHER;
       if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
-      if (const char* e = std::getenv("MAD_BREC")) brec_on = e[0] != '0';
       L.brec = (dim == 3 && l == 0 && brec_on);
       L.g.rs = ncoef_ + (L.brec ? 1 : 0);
       const int64_t cplane = L.g.sz * L.g.rs;
@@ -376,25 +352,6 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * ctot));
       HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
-      if ((dim == 3 && c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL && fusedg_wanted(c->d)) ||
-          (l + 1 < nl && rr_g_level(c, l, L))) {
-        const int64_t tplane = L.g.sz * 6;
-        const int64_t ttot = (L.g.nz + 2 * cgp) * tplane + 2 * margin * 6;
-        HIP_CHECK(hipMalloc(&L.ct_alloc, sizeof(T) * ttot));
-        HIP_CHECK(hipMemsetAsync(L.ct_alloc, 0, sizeof(T) * ttot, c->stream));
-        L.ct = L.ct_alloc + margin * 6 + cgp * tplane;
-      }
-      if (tsweep_level(c, l, L)) {
-        using TG = TSweepGeom;
-        const int64_t ntx = (L.g.nx + TG::TX - 1) / TG::TX, nty = (L.g.ny + TG::TY - 1) / TG::TY;
-        L.tg.tpitch = ntx * TG::TX + 2 * TG::PAD;
-        L.tg.trow = TG::NCOMP * L.tg.tpitch;
-        L.tg.tplane = (nty * TG::TY + 2 * TG::PAD) * L.tg.trow;
-        const int64_t ttot = (L.g.nz + 2 * (int64_t)GHOST) * L.tg.tplane;
-        HIP_CHECK(hipMalloc(&L.gt_alloc, sizeof(T) * ttot));
-        HIP_CHECK(hipMemsetAsync(L.gt_alloc, 0, sizeof(T) * ttot, c->stream));
-        L.gt = L.gt_alloc + (int64_t)GHOST * L.tg.tplane;
-      }
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
@@ -432,7 +389,7 @@ class Solver final : public SolverBase {
         // than a whole 64-plane rank sweep -- while an event after the short boundary
         // launch releases the exchange within ~0.05 ms, so boundary + interior
         // launches (parts 1, 2) win.
-        if (can_wait && (c->d.gs_kernel == 4 || c->d.gs_kernel == 6)) {
+        if (can_wait && c->d.gs_kernel == 4) {
           HIP_CHECK(hipExtMallocWithFlags((void**)&lv_[l].sig, 2 * sizeof(uint32_t),
                                           hipMallocSignalMemory));
           const uint32_t zero[2] = {0u, 0u};
@@ -525,30 +482,16 @@ class Solver final : public SolverBase {
   // level l's x changed without its ghost planes (they must be exchanged again)
   void x_changed(int l) { lv_[l].x_halo_ok = false; }
 
-  // target grid size of the z-marching transfer kernels (MAD_XFER_BLOCKS, tuning)
-  static int xfer_blocks() {
-    static const int v = [] {
-      const char* e = std::getenv("MAD_XFER_BLOCKS");
-      return e ? std::max(1, std::atoi(e)) : 1024;
-    }();
-    return v;
-  }
-
-  // element shift of the x / t arrays (MAD_X_SHIFT, tuning; must stay < margin)
-  static int64_t x_shift() {
-    static const int64_t v = [] {
-      const char* e = std::getenv("MAD_X_SHIFT");
-      return e ? (int64_t)std::max(0, std::min(64, std::atoi(e))) : (int64_t)0;
-    }();
-    return v;
-  }
+  // target grid size of the z-marching transfer kernels
+  static constexpr int XFER_BLOCKS = 1024;
+  static int xfer_blocks() { return XFER_BLOCKS; }
 
   // rows kept beyond the outermost plane of every level array (see setup)
   // (covers a tile region of up to 40 rows x 256 points hanging over the last plane)
   static int64_t margin_elems(const Geo& g) { return 48 * g.sy + 512; }
 
   bool use_fused(int l) const {
-    const int v = c_->d.gs_kernel;  // 0 auto (v3), 1 per-colour passes, 2 fused v2, 3 / 4 fused v3, 5 / 6 fused g-free
+    const int v = c_->d.gs_kernel;  // 0 auto, 1 per-colour passes, 3 / 4 fused
     if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL) return false;
     if (v == 1) return false;
     if (v >= 2) return true;
@@ -559,28 +502,17 @@ class Solver final : public SolverBase {
     return (int64_t)g.nx * g.ny * g.nz >= (int64_t)4 << 20 && g.nz >= 64;
   }
 
-  // fused-sweep launch configuration.  Defaults are the measured best at 512^3;
-  // MAD_FUSED_TILE (0 64x16/512, 1 64x32/1024, 2 128x16/1024, 3 128x8/512),
-  // MAD_FUSED_LEAD (prefetch lead in stages, 2 or 3) and MAD_FUSED_BLOCKS (target
-  // grid size) override them for tuning runs (full-tensor fp32/fp64 only).
+  // fused-sweep launch configuration, the measured best at 512^3 (profiles/r01_*): fp32 full
+  // tensor 64x32 tiles of 1024 threads (one block per CU, 93 KB LDS), ~256 blocks (one round,
+  // z-chunks of 256 planes: least chunk-overlap re-reads); fp64 full tensor 64x16 / 512 (the
+  // 64x32 ring would need 186 KB of LDS); diagonal / isotropic tensors 64x16 / 1024
   struct FusedCfg {
-    int tile = 0, lead = 2, blocks = 2048;
+    int blocks = 2048;
   };
-  // fp32 full tensor: 64x32 tiles of 1024 threads (one block per CU, 93 KB LDS),
-  // ~256 blocks; fp64 keeps 64x16/512 (the 64x32 ring would need 186 KB of LDS)
-  static const FusedCfg& fused_cfg() {
-    static FusedCfg c = [] {
-      FusedCfg f;
-      if (sizeof(T) == 4) {
-        f.tile = 1;
-        f.blocks = 256;  // one round, z-chunks of 256 planes at 512^3: least chunk-overlap re-reads
-      }
-      if (const char* e = std::getenv("MAD_FUSED_TILE")) f.tile = std::atoi(e);
-      if (const char* e = std::getenv("MAD_FUSED_LEAD")) f.lead = std::atoi(e);
-      if (const char* e = std::getenv("MAD_FUSED_BLOCKS")) f.blocks = std::max(1, std::atoi(e));
-      return f;
-    }();
-    return c;
+  static FusedCfg fused_cfg() {
+    FusedCfg f;
+    if (sizeof(T) == 4) f.blocks = 256;
+    return f;
   }
 
   // z-range of one fused launch: chunks q = 0..nchunks-1 cover owned planes
@@ -601,116 +533,14 @@ class Solver final : public SolverBase {
   // 3 whole slab with the last chunk marched downward and the edge-plane signals
   // (single-launch rank-slab sweep); gs_kernel 4 runs part 0 with the downward last
   // chunk (no signals)
-  // full-tensor sweeps with g recomputed in-kernel (gs_fusedg_k, tensor records L.ct):
-  // gs_kernel 5 / 6, or MAD_FUSEDG=1 for the fused forms 0 / 3 / 4 (A/B runs).  Not the
-  // default: it moves the 36 algorithmic bytes instead of 48, but its pending records
-  // (~250 VGPRs per thread) leave 2 waves per SIMD and it runs latency-bound
-  static bool fusedg_env() {
-    static const bool v = [] {
-      const char* e = std::getenv("MAD_FUSEDG");
-      return e && e[0] == '1';
-    }();
-    return v;
-  }
-  // V-cycle descent with g recomputed from the tensor records (resid_restrict3g_k: 32
-  // instead of 44 B per fine voxel): full 3D tensor, V-cycle / FMG solves, levels the
-  // one-pass residual + restriction runs on and whose records carry no b.  Opt-in
-  // (MAD_RR_G=1, measurement runs): bit-identical, but it issues 2.1x the VALU / LDS / SALU
-  // instructions of resid_restrict3_k and runs 1.2-1.5x slower at 512^3 (DESIGN.md,
-  // profiles/r02_rr_g_ab.md)
-  // the one-pass descent on rank slabs (MAD_RR_SLAB=0: residual + exchange + restriction
-  // there, A/B runs)
-  static bool rr_slab_env() {
-    static const bool v = [] {
-      const char* e = std::getenv("MAD_RR_SLAB");
-      return !(e && e[0] == '0');
-    }();
-    return v;
-  }
-  static bool rr_g_env() {
-    static const bool v = [] {
-      const char* e = std::getenv("MAD_RR_G");
-      return e && e[0] == '1';
-    }();
-    return v;
-  }
-  static bool rr_g_level(const mad_ctx* c, int l, const LevelData<T>& L) {
-    const LevelGeom& G = c->geom[l];
-    return rr_g_env() && c->dim == 3 && c->kind == KFULL && c->d.cycle != MAD_SMOOTHER && !L.brec &&
-           !G.distributed && !c->geom[l + 1].distributed && L.g.nx >= 16 && L.g.ny >= 16 &&
-           L.g.nz >= 2;
-  }
-  static bool fusedg_wanted(const mad_desc& d) {
-    return d.gs_kernel == 5 || d.gs_kernel == 6 ||
-           (fusedg_env() && (d.gs_kernel == 0 || d.gs_kernel == 3 || d.gs_kernel == 4));
-  }
-  bool fusedg_on(const LevelData<T>& L) const {
-    return L.ct != nullptr && c_->kind == KFULL && fusedg_wanted(c_->d);
-  }
-  // the g-free level sweep gs_tsweep_k (fp32 full tensor; 36 instead of 48 B per voxel-sweep):
-  // gs_kernel 7, on the levels the fused sweep runs (3D, >= 4 M voxels, >= 64 planes)
-  static bool tsweep_level(const mad_ctx* c, int l, const LevelData<T>& L) {
-    (void)l;
-    if (!(sizeof(T) == 4 && c->dim == 3 && c->kind == KFULL && c->d.smoother == MAD_GAUSS_SEIDEL))
-      return false;
-    if (c->d.gs_kernel == 7) return true;  // every 3D level (parity tests)
-    return false;
-  }
-  bool tsweep_on(const LevelData<T>& L) const { return L.gt != nullptr; }
-  void launch_tsweep(LevelData<T>& L, int part) {
-    if constexpr (sizeof(T) == 4) {
-      using TG = TSweepGeom;
-      const int ntx = (L.g.nx + TG::TX - 1) / TG::TX, nty = (L.g.ny + TG::TY - 1) / TG::TY;
-      const int tiles = ntx * nty;
-      FusedCfg fc;
-      fc.blocks = 256;  // one workgroup per CU (155 KB of LDS), one round
-      int flip = 0;
-      uint32_t* sig = nullptr;
-      const ZRange zr = part_range(L, tiles, fc, part, &flip, &sig);
-      REQUIRE(flip == 0 && sig == nullptr, MAD_ERR_UNSUPPORTED, "gs_tsweep_k marches upward only");
-      static bool attr = false;
-      if (!attr) {
-        HIP_CHECK(hipFuncSetAttribute((const void*)gs_tsweep_k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      TG::LDS_BYTES));
-        attr = true;
-      }
-      hipLaunchKernelGGL(gs_tsweep_k, dim3((unsigned)(tiles * zr.nchunks)), dim3(TG::NT), TG::LDS_BYTES,
-                         c_->stream, L.x, L.t, L.b, L.gt, L.g, L.tg, zr.zc, ntx, nty, zr.zbase, zr.zstride);
-    } else {
-      (void)L;
-      (void)part;
-      throw MadError(MAD_ERR_UNSUPPORTED, "gs_tsweep_k is fp32 only");
-    }
-  }
-  // gs_fusedg_k tile: fp32 64x16 (432 blocks of 2x2 points, 512 threads, 2 waves per
-  // SIMD for ~200 VGPRs of records in flight), 32x32 (MAD_FUSEDG_TILE=1) or 32x16 on 256
-  // threads, two workgroups per CU (MAD_FUSEDG_TILE=2); fp64 32x16 on 256 threads (one wave
-  // per SIMD)
-  static int fusedg_tile() {
-    static const int v = [] {
-      const char* e = std::getenv("MAD_FUSEDG_TILE");
-      return e ? std::atoi(e) : 0;
-    }();
-    return v;
-  }
-  void fusedg_dims(int* tx, int* ty, int* nt) const {
-    if (sizeof(T) == 8) {
-      *tx = 32; *ty = 16; *nt = 256;
-    } else if (fusedg_tile() == 1) {
-      *tx = 32; *ty = 32; *nt = 512;
-    } else if (fusedg_tile() == 2) {
-      *tx = 32; *ty = 16; *nt = 256;
-    } else {
-      *tx = 64; *ty = 16; *nt = 512;
-    }
-  }
-
-  // z-chunks of one launch of `part` (see launch_fused) over `tiles` tiles per plane
+  // z-chunks of one launch of `part` over `tiles` tiles per plane: the whole slab, or the
+  // two boundary chunks of a rank slab (they produce the halo planes), or the interior
+  // between them
   ZRange part_range(LevelData<T>& L, int tiles, const FusedCfg& fc, int part, int* flip,
                     uint32_t** sig) {
     const int nz = L.g.nz;
     ZRange zr = whole_range(nz, tiles, fc);
-    *flip = ((c_->d.gs_kernel == 4 || c_->d.gs_kernel == 6) && part == 0) ? 1 : 0;
+    *flip = (c_->d.gs_kernel == 4 && part == 0) ? 1 : 0;
     *sig = nullptr;
     if (part == 3) {
       REQUIRE(zr.nchunks >= 2 && zr.zc >= GHOST, MAD_ERR_UNSUPPORTED, "slab too thin for the single-launch sweep");
@@ -720,177 +550,62 @@ class Solver final : public SolverBase {
       zr = ZRange{0, boundary_planes(), nz - boundary_planes(), 2};
     } else if (part == 2) {
       const int ni = nz - 2 * boundary_planes();
-      static const int iblocks = [&] {
-        const char* e = std::getenv("MAD_INTERIOR_BLOCKS");  // tuning runs only
-        return e ? std::max(1, std::atoi(e)) : fc.blocks;
-      }();
-      int chunks = std::max(1, std::min((iblocks + tiles - 1) / tiles, std::max(1, ni / 16)));
+      int chunks = std::max(1, std::min((fc.blocks + tiles - 1) / tiles, std::max(1, ni / 16)));
       const int zc = (ni + chunks - 1) / chunks;
       zr = ZRange{boundary_planes(), zc, zc, (ni + zc - 1) / zc};
     }
     return zr;
   }
 
-  template <int TX, int TY, int NT, int MINW = NT / 256>
-  void launch_fusedg(LevelData<T>& L, int part) {
+  template <int KD, int TX, int TY, int NT>
+  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
-    FusedCfg fc;
-    fc.blocks = 256 * (MINW * 256 / NT);  // one round of the workgroups a CU holds
-    if (const char* e = std::getenv("MAD_FUSED_BLOCKS")) fc.blocks = std::max(1, std::atoi(e));
     int flip = 0;
     uint32_t* sig = nullptr;
     const ZRange zr = part_range(L, tiles, fc, part, &flip, &sig);
-    using FG = FusedGGeom<TX, TY>;
-    constexpr size_t lds = sizeof(T) * FG::ELEMS;
-    static_assert(lds <= 160 * 1024, "gs_fusedg_k tile exceeds the LDS");
-    auto kern = gs_fusedg_k<T, TX, TY, NT, MINW>;
-    static bool attr = false;
-    if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr = true;
-    }
-    REQUIRE(L.g.nx >= 3 && L.g.ny >= 3 && L.g.nz >= 3, MAD_ERR_UNSUPPORTED, "fused sweep needs >= 3 points per axis");
-    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * zr.nchunks)), dim3(NT), lds, c_->stream, L.x, L.t, L.b,
-                       L.ct, L.g, zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig);
-  }
-
-  template <int KD, int TX, int TY, int NT>
-  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part, bool prolong = false) {
-    const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
-    const int tiles = ntx * nty;
-    const int nz = L.g.nz;
-    ZRange zr = whole_range(nz, tiles, fc);
-    int flip = ((c_->d.gs_kernel == 4 || c_->d.gs_kernel == 6) && part == 0) ? 1 : 0;
-    uint32_t* sig = nullptr;
-    if (part == 3) {
-      zr = whole_range(nz, tiles, fc);
-      REQUIRE(zr.nchunks >= 2 && zr.zc >= GHOST, MAD_ERR_UNSUPPORTED, "slab too thin for the single-launch sweep");
-      flip = 1;
-      sig = L.sig;
-    } else if (part == 1) {  // the two boundary chunks of a rank slab (they produce the halo planes)
-      zr = ZRange{0, boundary_planes(), nz - boundary_planes(), 2};
-    } else if (part == 2) {  // the interior between them
-      const int ni = nz - 2 * boundary_planes();
-      static const int iblocks = [&] {
-        const char* e = std::getenv("MAD_INTERIOR_BLOCKS");  // tuning runs only
-        return e ? std::max(1, std::atoi(e)) : fc.blocks;
-      }();
-      int chunks = std::max(1, std::min((iblocks + tiles - 1) / tiles, std::max(1, ni / 16)));
-      const int zc = (ni + chunks - 1) / chunks;
-      zr = ZRange{boundary_planes(), zc, zc, (ni + zc - 1) / zc};
-    }
     const unsigned nb = (unsigned)(tiles * zr.nchunks);
-    if (c_->d.gs_kernel == 2) {
-      REQUIRE(part == 0, MAD_ERR_UNSUPPORTED, "fused v2 sweeps the whole slab");
-      hipLaunchKernelGGL((gs_fused_k<T, KD, 64, 16, (KD == KFULL ? 512 : 1024), (sizeof(T) == 8 ? 2 : 4)>),
-                         dim3((unsigned)(((L.g.nx + 63) / 64) * ((L.g.ny + 15) / 16) * zr.nchunks)),
-                         dim3(KD == KFULL ? 512 : 1024), 0, c_->stream, L.x, L.t, L.b, L.cf, L.g,
-                         L.rat, zr.zc, (L.g.nx + 63) / 64, (L.g.ny + 15) / 16);
-      return;
-    }
     constexpr int NC = (KD == KFULL) ? 4 : 2;
     using FG = FusedGeom<NC, TX, TY>;
     constexpr size_t lds = sizeof(T) * FG::NP * FG::PLANE;
-    // PROLONG: + the 4-slot coarse ring (gs_fused3_k)
-    constexpr size_t lds_p = lds + sizeof(T) * 4 * (FG::RX / 2 + 3) * (FG::RY / 2 + 3);
     REQUIRE(lds <= 160 * 1024, MAD_ERR_UNSUPPORTED,
             "fused GS tile needs " + std::to_string(lds) + " B of LDS (> 160 KiB)");
     // fp64 doubles the register footprint: 2 waves per SIMD (one 512-thread block per CU,
     // which is all its LDS allows anyway)
     constexpr int MW = sizeof(T) == 8 ? 2 : 4;
-    ProlongArgs<T> pa{};
-    auto run = [&](auto kern, size_t bytes) {
-      static bool attr = false;
-      if (!attr) {
+    auto run = [&](auto kern) {
+      // every instance that can be launched gets its dynamic-LDS opt-in (a kernel pointer
+      // set, not one flag per function type: several instances share one signature)
+      static std::vector<const void*> attr;
+      if (std::find(attr.begin(), attr.end(), (const void*)kern) == attr.end()) {
         HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)bytes));
-        attr = true;
+                                      (int)lds));
+        attr.push_back((const void*)kern);
       }
-      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), bytes, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, pa);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
+                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig);
     };
-    if (prolong) {
-      // the first post-smoothing sweep of a V-cycle with x + P e_c folded into its loads
-      // (prolong_fold_ok: one rank, whole slab, the default full-tensor tile)
-      REQUIRE(part == 0 && flip == 0 && !L.brec, MAD_ERR_STATE, "prolongation fold on a plain sweep only");
-      if constexpr (KD == KFULL && ((sizeof(T) == 4 && TX == 64 && TY == 32 && NT == 1024) ||
-                                    (sizeof(T) == 8 && TX == 64 && TY == 16 && NT == 512))) {
-        const LevelData<T>& C = *(&L + 1);
-        REQUIRE(C.g.nx == (C.cent[0] ? L.g.nx / 2 : (L.g.nx + 1) / 2) &&
-                    C.g.ny == (C.cent[1] ? L.g.ny / 2 : (L.g.ny + 1) / 2) &&
-                    C.g.nz == (C.cent[2] ? L.g.nz / 2 : (L.g.nz + 1) / 2) && C.g.sy == C.g.nx,
-                MAD_ERR_STATE, "prolongation fold: unexpected coarse geometry");
-        pa = ProlongArgs<T>{C.x, (C.cent[0] ? 1 : 0) | (C.cent[1] ? 2 : 0) | (C.cent[2] ? 4 : 0)};
-        run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>, lds_p);
-        return;
-      }
-      throw MadError(MAD_ERR_STATE, "prolongation fold: no kernel for this tile");
-    }
     if (L.brec)
-      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>, lds);
-    else if (KD == KFULL && fc.lead == 3)
-      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 3>, lds);
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
     else
-      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>, lds);
+      run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
   }
-
 
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
   void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {
-    if (tsweep_on(L)) {
-      FusedCfg fc;
-      fc.blocks = 256;
-      *tiles = ((L.g.nx + TSweepGeom::TX - 1) / TSweepGeom::TX) * ((L.g.ny + TSweepGeom::TY - 1) / TSweepGeom::TY);
-      *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
-      return;
-    }
-    if (fusedg_on(L)) {
-      int tx, ty, nt;
-      fusedg_dims(&tx, &ty, &nt);
-      FusedCfg fc;
-      fc.blocks = (sizeof(T) == 4 && fusedg_tile() == 2) ? 512 : 256;
-      if (const char* e = std::getenv("MAD_FUSED_BLOCKS")) fc.blocks = std::max(1, std::atoi(e));
-      *tiles = ((L.g.nx + tx - 1) / tx) * ((L.g.ny + ty - 1) / ty);
-      *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
-      return;
-    }
-    const FusedCfg& fc = fused_cfg();
-    int tx = 64, ty = 16;
-    if (c_->kind == KFULL) {
-      if (fc.tile == 1) ty = 32;
-      if (fc.tile == 2) tx = 128;
-      if (fc.tile == 3) { tx = 128; ty = 8; }
-    }
+    const FusedCfg fc = fused_cfg();
+    const int tx = 64, ty = (c_->kind == KFULL && sizeof(T) == 4) ? 32 : 16;
     *tiles = ((L.g.nx + tx - 1) / tx) * ((L.g.ny + ty - 1) / ty);
     *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
   }
 
-  void launch_fused_part(LevelData<T>& L, int part, bool prolong = false) {
-    const FusedCfg& fc = fused_cfg();
-    if (tsweep_on(L)) {
-      REQUIRE(!prolong, MAD_ERR_STATE, "prolongation fold: not with gs_tsweep_k");
-      launch_tsweep(L, part);
-    } else if (fusedg_on(L)) {
-      if constexpr (sizeof(T) == 8) {
-        launch_fusedg<32, 16, 256>(L, part);
-      } else {
-        if (fusedg_tile() == 1)
-          launch_fusedg<32, 32, 512>(L, part);
-        else if (fusedg_tile() == 2)
-          launch_fusedg<32, 16, 256, 2>(L, part);
-        else
-          launch_fusedg<64, 16, 512>(L, part);
-      }
-    } else if (c_->kind == KFULL) {
-      if (fc.tile == 1)
-        launch_fused<KFULL, 64, 32, 1024>(L, fc, part, prolong);
-      else if (fc.tile == 2)
-        launch_fused<KFULL, 128, 16, 1024>(L, fc, part, prolong);
-      else if (fc.tile == 3)
-        launch_fused<KFULL, 128, 8, 512>(L, fc, part, prolong);
+  void launch_fused_part(LevelData<T>& L, int part) {
+    const FusedCfg fc = fused_cfg();
+    if (c_->kind == KFULL) {
+      if constexpr (sizeof(T) == 4)
+        launch_fused<KFULL, 64, 32, 1024>(L, fc, part);
       else
-        launch_fused<KFULL, 64, 16, 512>(L, fc, part, prolong);
+        launch_fused<KFULL, 64, 16, 512>(L, fc, part);
     } else if (c_->kind == KDIAG) {
       launch_fused<KDIAG, 64, 16, 1024>(L, fc, part);
     } else {
@@ -915,38 +630,13 @@ class Solver final : public SolverBase {
       std::snprintf(buf, sizeof buf, "gs_lex_plane_k<%s, %d, %d>", tn, dim, kind);
     } else if (!use_fused(l)) {
       std::snprintf(buf, sizeof buf, "gs_color_k<%s, %d, %d>", tn, dim, kind);
-    } else if (c_->d.gs_kernel == 2) {
-      std::snprintf(buf, sizeof buf, "gs_fused_k<%s, %d, 64, 16, %d, %d>", tn, kind,
-                    kind == KFULL ? 512 : 1024, sizeof(T) == 8 ? 2 : 4);
-    } else if (tsweep_on(lv_[l])) {
-      std::snprintf(buf, sizeof buf, "gs_tsweep_k");
-      if (sweep_overlap(l)) return std::string(buf) + " [rank slab: boundary + interior launches]";
-    } else if (fusedg_on(lv_[l])) {
-      int tx, ty, nt;
-      fusedg_dims(&tx, &ty, &nt);
-      std::snprintf(buf, sizeof buf, "gs_fusedg_k<%s, %d, %d, %d%s>", tn, tx, ty, nt,
-                    (sizeof(T) == 4 && fusedg_tile() == 2) ? ", 2" : "");
-      const LevelData<T>& L = lv_[l];
-      if (sweep_overlap(l)) {
-        int tiles = 0, nchunks = 0;
-        fused_shape(L, &tiles, &nchunks);
-        const bool single = L.sig && nchunks >= 2;
-        return std::string(buf) + (single ? " [rank slab: single launch, edge signals]"
-                                          : " [rank slab: boundary + interior launches]");
-      }
     } else {
-      const FusedCfg& fc = fused_cfg();
-      int tx = 64, ty = 16, nt = kind == KFULL ? 512 : 1024;
-      if (kind == KFULL) {
-        if (fc.tile == 1) { tx = 64; ty = 32; nt = 1024; }
-        if (fc.tile == 2) { tx = 128; ty = 16; nt = 1024; }
-        if (fc.tile == 3) { tx = 128; ty = 8; nt = 512; }
-      }
+      const int tx = 64, ty = (kind == KFULL && sizeof(T) == 4) ? 32 : 16;
+      const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : 1024;
       const bool brec = lv_[l].brec;
-      const int lead = (!brec && kind == KFULL && fc.lead == 3) ? 3 : 2;
-      // every template argument, as rocprofv3 prints the instantiation (BREC, PROLONG last)
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, %d, %s, false>", tn, kind, tx,
-                    ty, nt, sizeof(T) == 8 ? 2 : 4, lead, brec ? "true" : "false");
+      // every template argument, as rocprofv3 prints the instantiation (BREC last)
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s>", tn, kind, tx, ty, nt,
+                    sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false");
       // rank slabs: which sweep form fused_sweep takes
       const LevelData<T>& L = lv_[l];
       if (sweep_overlap(l)) {
@@ -986,17 +676,12 @@ class Solver final : public SolverBase {
   // (2 chunks x tiles per plane >= 128 workgroups): on smaller levels the split's short,
   // under-filled boundary launch costs more than the exchange it hides (a 256^2-plane level
   // at 2 ranks: 56 + 102 us per sweep split, profiles/r02_rank_vcycle.md), so they sweep in
-  // one launch and exchange afterwards.  MAD_SWEEP_OVERLAP=1 forces the split (A/B runs).
+  // one launch and exchange afterwards.
   bool sweep_overlap(int l) const {
     const LevelData<T>& L = lv_[l];
-    if (!(c_->comm.active() && c_->geom[l].distributed && c_->d.gs_kernel != 2 &&
-          L.g.nz >= 3 * boundary_planes()))
+    if (!(c_->comm.active() && c_->geom[l].distributed && L.g.nz >= 3 * boundary_planes()))
       return false;
-    static const bool force = [] {
-      const char* e = std::getenv("MAD_SWEEP_OVERLAP");
-      return e && e[0] == '1';
-    }();
-    if (force || c_->d.gs_kernel != 0) return true;
+    if (c_->d.gs_kernel != 0) return true;
     int tiles = 0, nchunks = 0;
     fused_shape(L, &tiles, &nchunks);
     return 2 * tiles >= 128;
@@ -1014,7 +699,7 @@ class Solver final : public SolverBase {
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
-    if (L.brec && c_->d.gs_kernel != 2 && !fusedg_on(L) && !tsweep_on(L)) {
+    if (L.brec) {
       sync_brec(l);
     } else if (!L.b_halo_ok) {
       halo(l, L.b, GHOST);
@@ -1040,16 +725,7 @@ class Solver final : public SolverBase {
                                std::is_same<T, double>::value, c_->comm_stream);
       HIP_CHECK(hipEventRecord(L.ev_halo, c_->comm_stream));
     } else if (!overlap) {
-      // MAD_SPLIT_PROXY=1 (measurement only): launch a single-GPU slab as a rank slab's
-      // boundary + interior parts, without the exchange (tools/bench_slab.py)
-      static const bool proxy = std::getenv("MAD_SPLIT_PROXY") != nullptr;
-      if (prolong_l_ == l) {  // the V-cycle's correction, folded into this sweep's loads
-        prolong_l_ = -1;
-        launch_fused_part(L, 0, true);
-      } else if (proxy && c_->d.gs_kernel != 2 && L.g.nz >= 3 * boundary_planes()) {
-        launch_fused_part(L, 1);
-        launch_fused_part(L, 2);
-      } else {
+      {
         launch_fused_part(L, 0);
       }
     } else {
@@ -1112,14 +788,9 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipGetLastError());
   }
 
-  // per-colour GS on a 3D rank slab with one halo exchange per sweep (MAD_COLOUR_CA=0:
-  // one exchange per colour, A/B runs)
+  // per-colour GS on a 3D rank slab with one halo exchange per sweep
   bool colour_ca(int l) const {
-    static const bool env = [] {
-      const char* e = std::getenv("MAD_COLOUR_CA");
-      return !(e && e[0] == '0');
-    }();
-    return env && c_->dim == 3 && c_->comm.active() && c_->geom[l].distributed &&
+    return c_->dim == 3 && c_->comm.active() && c_->geom[l].distributed &&
            c_->ncolors <= GHOST;
   }
 
@@ -1309,24 +980,18 @@ class Solver final : public SolverBase {
   // b[l+1] <- R (b[l] - A x[l]) in one pass (resid_restrict3_k, bit-identical to the
   // residual + restriction pair; r[l] is not written).  3D levels held whole by this
   // rank (one GPU, or the replicated coarse levels); false: not applicable, the caller
-  // runs residual + restriction.  MAD_FUSED_RR=0 turns it off (A/B runs).
+  // runs residual + restriction.
   bool residual_restrict(int l) override { return resid_restrict(l); }
   // zero_x: also zero x[l+1] (the V-cycle descent's fill, folded into the same pass)
   bool resid_restrict(int l, bool zero_x = false) {
-    static const bool on = [] {
-      const char* e = std::getenv("MAD_FUSED_RR");
-      return !(e && e[0] == '0');
-    }();
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
     // one GPU (or a replicated level), or a rank slab whose coarse level is a slab too (the
     // taps past the slab residualise the fine ghost planes: x and b ghost planes made current
     // first -- the b exchange stands in for the residual's)
     const bool dist = c_->geom[l].distributed;
-    if (!on || c_->dim != 3 || dist != c_->geom[l + 1].distributed || F.g.nx < 16 || F.g.ny < 16 ||
-        F.g.nz < 2)
+    if (c_->dim != 3 || dist != c_->geom[l + 1].distributed || F.g.nx < 16 || F.g.ny < 16 || F.g.nz < 2)
       return false;
-    if (dist && !rr_slab_env()) return false;
     if (dist) {
       halo(l, F.x, GHOST);
       if (!F.brec && !F.b_halo_ok) {
@@ -1338,50 +1003,10 @@ class Solver final : public SolverBase {
     C.b_halo_ok = C.brec_ok = false;
     T* zx = zero_x ? C.x : nullptr;
     if (zero_x) x_changed(l + 1);
-    static const int target = [] {
-      const char* e = std::getenv("MAD_RR_BLOCKS");  // tuning runs only
-      return e ? std::max(1, std::atoi(e)) : 1024;
-    }();
-    if (F.ct && !F.brec && c_->kind == KFULL && rr_g_env()) {
-      constexpr int CX = 32, CY = 8;
-      // MAD_RR_G_OCC (tuning runs): 1 caps registers at 128 for two 512-thread blocks per
-      // CU, 0 leaves them uncapped (one block per CU), 2: one 1024-thread block per CU
-      static const int occ = [] {
-        const char* e = std::getenv("MAD_RR_G_OCC");
-        return e ? std::atoi(e) : 1;
-      }();
-      const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
-      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / 4));
-      const int kc = (C.g.nz + chunks - 1) / chunks;
-      chunks = (C.g.nz + kc - 1) / kc;
-      const dim3 grid((unsigned)(ntx * nty * chunks));
-      auto go = [&](auto NTc, auto W) {
-        constexpr int NT = decltype(NTc)::value;
-        hipLaunchKernelGGL((resid_restrict3g_k<T, CX, CY, NT, decltype(W)::value>), grid, dim3(NT), 0,
-                           c_->stream, F.x, F.b, F.ct, F.g, C.b, zx, C.g, C.cent[0], C.cent[1],
-                           C.cent[2], kc, ntx);
-      };
-      using I512 = std::integral_constant<int, 512>;
-      if constexpr (sizeof(T) == 4) {
-        if (occ == 1) go(I512{}, std::integral_constant<int, 4>{});
-        else if (occ == 2) go(std::integral_constant<int, 1024>{}, std::integral_constant<int, 4>{});
-        else go(I512{}, std::integral_constant<int, 1>{});
-      } else {
-        go(I512{}, std::integral_constant<int, 1>{});  // 151 KB of LDS: one block per CU anyway
-      }
-      HIP_CHECK(hipGetLastError());
-      return true;
-    }
-    static const int tile = [] {
-      const char* e = std::getenv("MAD_RR_TILE");  // tuning runs only: 0 32x8, 1 32x16 coarse
-      return e ? std::atoi(e) : 0;
-    }();
-    // 512-thread blocks, two per CU (one block's barriers overlap the other's loads):
-    // 1.133 vs 1.177 ms per 512^3 launch at 1024 blocks (profiles/r01_rr_nt_prof.log)
-    static const int nt = [] {
-      const char* e = std::getenv("MAD_RR_NT");  // tuning runs only: 512 or 1024 threads
-      return e ? std::atoi(e) : 512;
-    }();
+    // 32 x 8 coarse tiles in 512-thread blocks, two per CU (one block's barriers overlap the
+    // other's loads), ~1024 blocks: 1.133 vs 1.177 ms per 512^3 launch with 1024-thread blocks
+    // (profiles/r01_rr_nt_prof.log, r01_rr_blocks_prof.log)
+    constexpr int target = 1024;
     const int ncz = (int)c_->geom[l + 1].n[2];  // global coarse nz (taps in global indices)
     auto run = [&](auto CXc, auto CYc, auto NTc) {
       constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = decltype(NTc)::value;
@@ -1405,15 +1030,8 @@ class Solver final : public SolverBase {
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
       else go(std::integral_constant<int, KISO>{});
     };
-    if (tile == 1)
-      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 16>{},
-          std::integral_constant<int, 1024>{});
-    else if (nt == 512)
-      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
-          std::integral_constant<int, 512>{});
-    else
-      run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
-          std::integral_constant<int, 1024>{});
+    run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
+        std::integral_constant<int, 512>{});
     HIP_CHECK(hipGetLastError());
     return true;
   }
@@ -1503,10 +1121,7 @@ class Solver final : public SolverBase {
       fill(l + 1, MAD_X, 0.0);  // MAD.hxx:415-416
     }
     vcycle_rec(l + 1);        // MAD.hxx:418-420
-    if (prolong_fold_ok(l))   // MAD.hxx:422-435: x += P x_c inside the first post-sweep
-      prolong_l_ = l;
-    else
-      interpolate_up(l, true);
+    interpolate_up(l, true);  // MAD.hxx:422-435
     if (c_->d.verbose) verbose_line(l, 0, "initial");
     if (c_->d.verbose) {
       for (unsigned n = 0; n < nu; ++n) {
@@ -1576,15 +1191,11 @@ class Solver final : public SolverBase {
   // capture left behind is re-applied after every replay.  The first multi-rank cycle
   // runs eagerly (RCCL connects its peers lazily, outside any capture).  The
   // in-process LOCAL transport synchronises on the host and stays eager, as does the
-  // wait-on-value single-launch sweep (gs_kernel 4); MAD_VGRAPH_RANKS=0 disables the
-  // multi-rank graph.
+  // wait-on-value single-launch sweep (gs_kernel 4); mad_desc.options MAD_OPT_EAGER_RANK_VCYCLE
+  // keeps the multi-rank V-cycle eager (the reference for the graph-replay parity test).
   bool vgraph_ranks_ok() const {
-    static const bool env_ok = [] {
-      const char* e = std::getenv("MAD_VGRAPH_RANKS");
-      return !(e && e[0] == '0');
-    }();
-    return env_ok && (c_->comm.mode() == Comm::RCCL || c_->comm.mode() == Comm::SOLO) &&
-           c_->d.gs_kernel != 4 && c_->d.gs_kernel != 6;
+    return !(c_->d.options & MAD_OPT_EAGER_RANK_VCYCLE) &&
+           (c_->comm.mode() == Comm::RCCL || c_->comm.mode() == Comm::SOLO) && c_->d.gs_kernel != 4;
   }
 
   struct HaloFlags {
@@ -1719,28 +1330,6 @@ class Solver final : public SolverBase {
 
   void vcycle() override { vcycle_fast(); }
 
-  // The V-cycle's prolongation + add folded into level l's first post-smoothing sweep
-  // (gs_fused3_k<..., PROLONG>): one rank, full tensor, the fused sweep in its default tile on
-  // a whole slab (gs_kernel 0 / 3), no verbose trace (it prints the norm of the corrected x
-  // before smoothing).  Bit-identical to interp3_k + the sweep (test_prolongation_fold_is_bitwise).
-  // Opt-in (MAD_PROLONG_FOLD=1, measurement runs): the sweep kernel is at the SGPR limit
-  // already, the fold's uniform state spills (23 SGPR / 14 VGPR), and the folded level-0 +
-  // level-1 sweeps took 2.01 ms per cycle against 1.47 + 0.30 ms for the sweeps + interp3_k
-  // (profiles/r02_prolong_fold_ab.md).
-  int prolong_l_ = -1;
-  bool prolong_fold_ok(int l) const {
-    static const bool env = [] {
-      const char* e = std::getenv("MAD_PROLONG_FOLD");
-      return e && e[0] == '1';
-    }();
-    const FusedCfg& fc = fused_cfg();
-    const int def_tile = sizeof(T) == 4 ? 1 : 0;
-    return env && c_->dim == 3 && !c_->comm.active() && !c_->d.verbose && c_->kind == KFULL &&
-           c_->d.smoother == MAD_GAUSS_SEIDEL && (c_->d.gs_kernel == 0 || c_->d.gs_kernel == 3) &&
-           c_->d.iterations_per_grid >= 1 && use_fused(l) && !fusedg_on(lv_[l]) && !tsweep_on(lv_[l]) &&
-           !lv_[l].brec &&
-           fc.tile == def_tile;
-  }
   void fmg() override { fmg_rec(0); }
 
   void verbose_line(int l, int it, const char* what) {
@@ -2138,8 +1727,6 @@ class Solver final : public SolverBase {
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
-      if (L.ct_alloc) (void)hipFree(L.ct_alloc);
-      if (L.gt_alloc) (void)hipFree(L.gt_alloc);
     }
     lv_.clear();
     for (auto& a : r64alloc_)
@@ -2312,23 +1899,6 @@ class Solver final : public SolverBase {
           HIP_CHECK(hipStreamSynchronize(c_->stream));
           HIP_CHECK(hipFree(full64));
         }
-      }
-      if (L.gt) {
-        // the g-free sweep's tensor array (with the face ghosts) from the finished records
-        const int p0 = -GHOST, p1 = L.g.nz + GHOST;
-        dim3 grt((unsigned)((L.g.nx + 2 + 63) / 64), (unsigned)((L.g.ny + 2 + 3) / 4), (unsigned)(p1 - p0));
-        if constexpr (sizeof(T) == 4)
-          hipLaunchKernelGGL((build_gt_k<T>), grt, BLK, 0, c_->stream, L.cf, L.g, L.gt, L.tg, p0);
-        HIP_CHECK(hipGetLastError());
-      }
-      if (L.ct) {
-        // tensor records of every allocated plane the coefficient records hold
-        const int p0 = L.g.zlo_ghost ? -GHOST : 0;
-        const int p1 = L.g.nz + (L.g.zhi_ghost ? GHOST : 0);
-        const int64_t n = (int64_t)(p1 - p0) * L.g.sz;
-        hipLaunchKernelGGL((pack_tensor_k<T>), dim3(flat_blocks(n)), dim3(256), 0, c_->stream, L.cf,
-                           L.ct, L.g.sz, L.g.rs, p0, n);
-        HIP_CHECK(hipGetLastError());
       }
       if (l == nl - 1) build_coarsest_matrix(fine);
     }
@@ -2660,6 +2230,9 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "bad precision");
     REQUIRE(d->nranks >= 1 && d->rank >= 0 && d->rank < d->nranks, MAD_ERR_INVALID,
             "bad rank / nranks");
+    REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
+            MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
+    REQUIRE((d->options & ~MAD_OPT_EAGER_RANK_VCYCLE) == 0, MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");
     c->d = *d;

@@ -236,12 +236,9 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     H[q] = base + q * N;
   }
   const double* h = v->d.spacing;
-  // MAD_VED_IIR_LINE=1 (A/B runs): ved_iir_k's one thread per line for every axis, each
-  // output marched on its own
-  static const bool line_walk = [] {
-    const char* e = std::getenv("MAD_VED_IIR_LINE");
-    return e && e[0] == '1';
-  }();
+  // MAD_VED_OPT_LINE_WALK (the parity reference): ved_iir_k's one thread per line for every
+  // axis, each output marched on its own
+  const bool line_walk = (v->d.options & MAD_VED_OPT_LINE_WALK) != 0;
   // SI: the z pass reads the fp64 image, the others the T volumes
   auto launch = [&](const IirPass& P, int axis, auto si) {
     using SI = decltype(si);
@@ -251,18 +248,10 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
                          nx, ny, nz);
     } else if (axis == 0) {
       // contiguous lines: one wave per 64 lines and output, LDS-staged row chunks
-      // chunk rows of one 128-B line (3.76 vs 4.15 ms per 512^3 fp32 pass with 64 B;
-      // MAD_VED_IIR_XC=0 for 64 B, measurement runs)
-      static const int wide = [] {
-        const char* e = std::getenv("MAD_VED_IIR_XC");
-        return e ? std::atoi(e) : 1;
-      }();
+      // chunk rows of one 128-B line (3.76 vs 4.15 ms per 512^3 fp32 pass with 64 B)
       if constexpr (std::is_same<SI, T>::value) {
         const dim3 gr((unsigned)((lines + 63) / 64), (unsigned)P.nout);
-        if (wide == 1)
-          hipLaunchKernelGGL((ved_iir_x_k<SI, T, 128 / (int)sizeof(T)>), gr, dim3(64), 0, st, P, nx, lines);
-        else
-          hipLaunchKernelGGL((ved_iir_x_k<SI, T, 64 / (int)sizeof(T)>), gr, dim3(64), 0, st, P, nx, lines);
+        hipLaunchKernelGGL((ved_iir_x_k<SI, T, 128 / (int)sizeof(T)>), gr, dim3(64), 0, st, P, nx, lines);
       }
     } else {
       // strided lines: the outputs sharing an input in one march, one launch per input

@@ -26,7 +26,8 @@ class VED:
                  scales=(0.300, 0.482, 0.775, 1.245, 2.000), iterations=1,
                  diffusion_iterations=5, cycle=C.VCYCLE, time_step=0.1, tolerance=1e-6,
                  diffusion_iterations_per_grid=2, verbose=False, smoother=C.GAUSS_SEIDEL,
-                 precision=C.PRECISION_AUTO, device=-1, nranks=1, rank=0, hessian="recursive"):
+                 precision=C.PRECISION_AUTO, device=-1, nranks=1, rank=0, hessian="recursive",
+                 options=0):
         if len(shape) != 3:
             raise ValueError("VED is 3D (itkVEDMultigridImageFilter.h:46)")
         if len(scales) > C.VED_MAX_SCALES:
@@ -53,6 +54,7 @@ class VED:
         # ComputeHessian operator: "recursive" (ITK's HessianRecursiveGaussianImageFilter, the
         # reference's, default) or "fir" (sampled Gaussian derivative taps)
         d.hessian = {"recursive": C.VED_HESSIAN_RECURSIVE, "fir": C.VED_HESSIAN_FIR}[hessian]
+        d.options = int(options)  # C.VED_OPT_LINE_WALK: the line-walk parity reference
         self.desc = d
         self.nranks, self.rank = int(nranks), int(rank)
         nz = self.shape[0]

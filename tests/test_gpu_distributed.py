@@ -33,7 +33,7 @@ def _multi(nranks, fn, T, **kw):
 
 @pytest.mark.parametrize("nranks", [2, 4])
 @pytest.mark.parametrize("smoother,gs_kernel,cycle", [(0, 0, 0), (0, 1, 0), (2, 0, 0), (0, 3, 0),
-                                                      (0, 3, 2), (0, 5, 0), (0, 5, 2)])
+                                                      (0, 3, 2)])
 def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle):
     """cycle 2 (SMOOTHER): level-0 records carry b (sync_brec on ghost planes)."""
     import multigridanisotropicdiffusion_amd as M
@@ -82,10 +82,10 @@ def test_distributed_filter_run_matches_single(nranks):
 
 
 @pytest.mark.parametrize("nranks", [2])
-@pytest.mark.parametrize("gs_kernel", [4, 6])
+@pytest.mark.parametrize("gs_kernel", [4])
 @pytest.mark.parametrize("cycle", [0, 2])
 def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel, cycle):
-    """gs_kernel 4 / 6 on rank slabs deep enough for two z-chunks per tile column (64 planes
+    """gs_kernel 4 on rank slabs deep enough for two z-chunks per tile column (64 planes
     per rank): the single-launch sweep -- the top chunk marches downward, the edge chunks
     signal their finished edge planes and the communication stream exchanges them while
     the sweep runs.  Results equal the single-rank run bit for bit (sweeps, V-cycles)."""

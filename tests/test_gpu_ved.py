@@ -82,39 +82,24 @@ def test_recursive_hessian_on_four_point_axes(M):
             assert relmax(H[q], ref[..., q]) < 1e-12, (shape, q)
 
 
-def test_recursive_hessian_passes_are_bitwise_the_line_walk(M, tmp_path):
+def test_recursive_hessian_passes_are_bitwise_the_line_walk(M):
     """The production recursive passes -- x through LDS row chunks (ved_iir_x_k, 16 points
     per chunk), z / y with the outputs sharing an input in one march (ved_iir_grp_k) --
-    equal ved_iir_k's one thread per line and output (MAD_VED_IIR_LINE=1, in a child
-    process) bit for bit: partial last chunks of 1..3 points (the anticausal edge formulas
-    span two chunks), exact multiples of the chunk, line counts off the 64-line wave, both
-    precisions."""
-    import subprocess
-    import sys
+    equal ved_iir_k's one thread per line and output (mad_ved_desc.options
+    MAD_VED_OPT_LINE_WALK) bit for bit: partial last chunks of 1..3 points (the anticausal
+    edge formulas span two chunks), exact multiples of the chunk, line counts off the 64-line
+    wave, both precisions."""
     shapes = [(4, 6, 33), (5, 4, 18), (6, 5, 19), (4, 4, 4), (7, 9, 64), (9, 11, 47)]
-    here = os.path.dirname(os.path.abspath(__file__))
     rng = np.random.default_rng(13)
-    imgs = [rng.normal(50.0, 20.0, size=sh) for sh in shapes]
-    for q, im in enumerate(imgs):
-        np.save(tmp_path / f"img{q}.npy", im)
-    code = ("import sys, numpy as np; sys.path.insert(0, %r)\n"
-            "import multigridanisotropicdiffusion_amd as M\n"
-            "for q in range(%d):\n"
-            "    im = np.load(%r + '/img%%d.npy' %% q)\n"
-            "    for p in ('FP32', 'FP64'):\n"
-            "        v = M.VED(im.shape, (0.7, 1.1, 0.9), precision=getattr(M, p))\n"
-            "        np.save(%r + '/h%%d_%%s.npy' %% (q, p), np.asarray(v.hessian(im, 1.3)))\n"
-            "        v.close()\n") % (os.path.dirname(here), len(shapes), str(tmp_path), str(tmp_path))
-    env = dict(os.environ, MAD_VED_IIR_LINE="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    for q, im in enumerate(imgs):
+    for sh in shapes:
+        im = rng.normal(50.0, 20.0, size=sh)
         for p in ("FP32", "FP64"):
-            v = M.VED(im.shape, (0.7, 1.1, 0.9), precision=getattr(M, p))
-            H = np.asarray(v.hessian(im, 1.3))
-            v.close()
-            ref = np.load(tmp_path / f"h{q}_{p}.npy")
-            assert np.array_equal(H, ref), (shapes[q], p, np.abs(H - ref).max())
+            H = {}
+            for opt in (0, M.capi.VED_OPT_LINE_WALK):
+                v = M.VED(im.shape, (0.7, 1.1, 0.9), precision=getattr(M, p), options=opt)
+                H[opt] = np.asarray(v.hessian(im, 1.3))
+                v.close()
+            assert np.array_equal(H[0], H[M.capi.VED_OPT_LINE_WALK]), (sh, p)
 
 
 def test_fir_hessian_filter_run_matches_oracle(M, oracle_mod):
