@@ -155,9 +155,18 @@ int mad_get_desc(const mad_ctx *ctx, mad_desc *out);
 
 /* SetDiffusionTensor (MAD.hxx:66-101): AoS symmetric tensors, ITK
  * SymmetricSecondRankTensor component order [xx,xy,xz,yy,yz,zz] (3D) /
- * [xx,xy,yy] (2D), dtype MAD_F32 or MAD_F64.  Copied (cast to fp64) at call time. */
+ * [xx,xy,yy] (2D), dtype MAD_F32 or MAD_F64, of the whole (global) grid.  Copied
+ * (cast to fp64) at call time; a rank of a z-slab decomposition copies only the
+ * planes it stores (mad_tensor_planes) and keeps them across setups. */
 int mad_set_tensor(mad_ctx *ctx, const void *host_aos, int32_t dtype);
 int mad_set_tensor_device(mad_ctx *ctx, const void *dev_aos, int32_t dtype);
+/* The global z planes [first, first + n) of the tensor this context stores: the whole
+ * grid on one rank, the rank's slab plus ghost planes (the operator build's stencil
+ * reach) on a z-slab rank.  mad_set_tensor_planes takes just those (or any covering
+ * range starting at first_plane), so no process has to hold the global tensor. */
+int mad_tensor_planes(const mad_ctx *ctx, int64_t *first_plane, int64_t *nplanes);
+int mad_set_tensor_planes(mad_ctx *ctx, const void *host_aos, int32_t dtype,
+                          int64_t first_plane, int64_t nplanes);
 
 /* Build the grids hierarchy, per-level operators and the coarsest-grid direct
  * solver (GH.hxx:30-204, DS.hxx:32-88).  Implicit in mad_run; explicit for the

@@ -35,7 +35,8 @@ VED_OPT_LINE_WALK = 1
 
 EXPORTS = (
     "mad_desc_init", "mad_max_depth", "mad_create", "mad_destroy", "mad_last_error",
-    "mad_get_desc", "mad_set_tensor", "mad_set_tensor_device", "mad_setup", "mad_run",
+    "mad_get_desc", "mad_set_tensor", "mad_set_tensor_device", "mad_tensor_planes",
+    "mad_set_tensor_planes", "mad_setup", "mad_run",
     "mad_run_device", "mad_get_step_stats", "mad_get_cycle_trace", "mad_num_levels", "mad_plan_level",
     "mad_level_info", "mad_upload",
     "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
@@ -182,6 +183,8 @@ def load():
         "mad_get_desc": ([vp, ctypes.POINTER(MadDesc)], i32),
         "mad_set_tensor": ([vp, vp, i32], i32),
         "mad_set_tensor_device": ([vp, vp, i32], i32),
+        "mad_tensor_planes": ([vp, i64p, i64p], i32),
+        "mad_set_tensor_planes": ([vp, vp, i32, ctypes.c_int64, ctypes.c_int64], i32),
         "mad_setup": ([vp], i32),
         "mad_run": ([vp, vp, i32, vp, i32, ctypes.POINTER(MadStats)], i32),
         "mad_run_device": ([vp, vp, i32, vp, i32, ctypes.POINTER(MadStats)], i32),

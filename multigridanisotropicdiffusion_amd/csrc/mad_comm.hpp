@@ -220,6 +220,60 @@ class Comm {
     group_->barrier();
   }
 
+  // One hop of a deep ghost exchange (ghost regions deeper than a slab, filled hop by hop): every
+  // rank sends its planes [D, D + d) down (received at [nz + D, nz + D + d) by rank - 1) and
+  // [nz - D - d, nz - D) up (received at [-D - d, -D) by rank + 1).  D = 0 is exchange_planes;
+  // hop h (D = (h - 1) nz, d <= nz) forwards the ghosts hop h - 1 brought in.  Read and written
+  // planes are disjoint, so the in-process transport pulls straight from the neighbours.
+  void shift_planes(void* a, int64_t plane, int nz, int D, int d, int has_lo, int has_hi, size_t esz,
+                    bool is_double, hipStream_t s) {
+    if (D == 0) {
+      exchange_planes(a, plane, nz, d, has_lo, has_hi, esz, is_double, s);
+      return;
+    }
+    char* base = (char*)a;
+    const size_t pb = (size_t)plane * esz;
+    char* send_dn = base + (size_t)D * pb;
+    char* recv_hi = base + (size_t)(nz + D) * pb;
+    char* send_up = base + (ptrdiff_t)(nz - D - d) * (ptrdiff_t)pb;
+    char* recv_lo = base - (ptrdiff_t)(D + d) * (ptrdiff_t)pb;
+    if (mode_ == RCCL) {
+      const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
+      const size_t cnt = (size_t)plane * d;
+      const int lo = (rank_ - 1 + nranks_) % nranks_, hi = (rank_ + 1) % nranks_;
+      NCCL_CHECK(ncclGroupStart());
+      if (has_lo) {
+        NCCL_CHECK(ncclSend(send_dn, cnt, dt, lo, comm_, s));
+        NCCL_CHECK(ncclRecv(recv_lo, cnt, dt, lo, comm_, s));
+      }
+      if (has_hi) {
+        NCCL_CHECK(ncclSend(send_up, cnt, dt, hi, comm_, s));
+        NCCL_CHECK(ncclRecv(recv_hi, cnt, dt, hi, comm_, s));
+      }
+      NCCL_CHECK(ncclGroupEnd());
+      return;
+    }
+    if (mode_ == SOLO) {  // the same bytes from this rank's own planes
+      if (has_lo) HIPC_CHECK(hipMemcpyAsync(recv_lo, send_up, d * pb, hipMemcpyDeviceToDevice, s));
+      if (has_hi) HIPC_CHECK(hipMemcpyAsync(recv_hi, send_dn, d * pb, hipMemcpyDeviceToDevice, s));
+      return;
+    }
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->ptr[rank_] = a;
+    group_->barrier();
+    if (has_lo) {
+      const char* nb = (const char*)group_->ptr[rank_ - 1];
+      HIPC_CHECK(hipMemcpyAsync(recv_lo, nb + (ptrdiff_t)(nz - D - d) * (ptrdiff_t)pb, d * pb,
+                                hipMemcpyDeviceToDevice, s));
+    }
+    if (has_hi) {
+      const char* nb = (const char*)group_->ptr[rank_ + 1];
+      HIPC_CHECK(hipMemcpyAsync(recv_hi, nb + (size_t)D * pb, d * pb, hipMemcpyDeviceToDevice, s));
+    }
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->barrier();
+  }
+
   void allreduce_sum_f64(double* p, size_t n, hipStream_t s) {
     if (mode_ == RCCL) {
       NCCL_CHECK(ncclAllReduce(p, p, n, ncclDouble, ncclSum, comm_, s));

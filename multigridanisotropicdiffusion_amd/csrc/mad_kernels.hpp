@@ -1631,30 +1631,32 @@ __global__ void __launch_bounds__(256) convert_int_k(const S* __restrict__ x, D*
 
 // ---------------------------------------------------------------------------
 // setup (fp64): AoS input tensor -> SoA, kind detection, coefficient fields
+// (n points; component c of point q at out[c * cs + q]: cs = n for a whole grid, the slab
+// array's component stride on a rank)
 template <typename S>
 __global__ void __launch_bounds__(256) aos_to_soa_k(const S* __restrict__ in, double* __restrict__ out,
-                                                    int64_t n, int ncomp) {
+                                                    int64_t n, int ncomp, int64_t cs) {
   for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
        q += (int64_t)gridDim.x * blockDim.x)
-    for (int c = 0; c < ncomp; ++c) out[c * n + q] = (double)in[q * ncomp + c];
+    for (int c = 0; c < ncomp; ++c) out[c * cs + q] = (double)in[q * ncomp + c];
 }
 
 // flags[0] += any off-diagonal != 0, flags[1] += any diagonal entries differ,
 // flags[2] += any entry non-finite (NaN / Inf: MAD_ERR_NUMERIC at setup)
-__global__ void __launch_bounds__(256) tensor_kind_k(const double* __restrict__ M, int64_t n, int dim,
-                                                     unsigned int* __restrict__ flags) {
+__global__ void __launch_bounds__(256) tensor_kind_k(const double* __restrict__ M, int64_t n, int64_t cs,
+                                                     int dim, unsigned int* __restrict__ flags) {
   unsigned int off = 0, aniso = 0, bad = 0;
   const int ncomp = dim * (dim + 1) / 2;
   for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
        q += (int64_t)gridDim.x * blockDim.x) {
     if (dim == 3) {
-      off |= (M[1 * n + q] != 0.0) | (M[2 * n + q] != 0.0) | (M[4 * n + q] != 0.0);
-      aniso |= (M[0 * n + q] != M[3 * n + q]) | (M[0 * n + q] != M[5 * n + q]);
+      off |= (M[1 * cs + q] != 0.0) | (M[2 * cs + q] != 0.0) | (M[4 * cs + q] != 0.0);
+      aniso |= (M[0 * cs + q] != M[3 * cs + q]) | (M[0 * cs + q] != M[5 * cs + q]);
     } else {
-      off |= (M[1 * n + q] != 0.0);
-      aniso |= (M[0 * n + q] != M[2 * n + q]);
+      off |= (M[1 * cs + q] != 0.0);
+      aniso |= (M[0 * cs + q] != M[2 * cs + q]);
     }
-    for (int c = 0; c < ncomp; ++c) bad |= !isfinite(M[c * n + q]);
+    for (int c = 0; c < ncomp; ++c) bad |= !isfinite(M[c * cs + q]);
   }
   if (__any(off) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
   if (__any(aniso) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1u);
@@ -1741,16 +1743,19 @@ __global__ void __launch_bounds__(256) build_coef_k(const double* __restrict__ M
 // reaches them) come from the previous iterations; in-plane neighbours and the one-sided
 // border formulas read memory as build_coef_k does.  Same arithmetic and order, so the
 // coefficients are bit-identical to build_coef_k's.
+// Global plane indices throughout: planes [kb, ke) of a level with nz planes are built; M and cf
+// point at global plane 0 (on a rank slab: the slab arrays shifted by their first global plane,
+// only planes [kb - 2, ke + 2) of M and [kb, ke) of cf are touched); cs is M's component stride.
 template <typename T, int KIND>
 __global__ void __launch_bounds__(256) build_coef3_k(const double* __restrict__ M, int nx, int ny,
                                                      int nz, CoefFactors f, T* __restrict__ cf,
-                                                     int rs, int kc) {
+                                                     int rs, int kc, int kb, int ke, int64_t cs) {
   using L = CoefLayout<3, KIND>;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
-  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, nz);
+  const int k0 = kb + blockIdx.z * kc, k1 = min(k0 + kc, ke);
   if (i >= nx || j >= ny || k0 >= k1) return;
-  const int64_t n = (int64_t)nx * ny * nz, sz = (int64_t)nx * ny;
+  const int64_t n = cs, sz = (int64_t)nx * ny;
   const int64_t col = i + (int64_t)nx * j;
   const int64_t orow = ((int64_t)nx * j + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1)));
   const int nn[3] = {nx, ny, nz};
@@ -1857,13 +1862,14 @@ __device__ __forceinline__ void g_combine(T dxax, T dyay, T dzaz, T dxexy, T dye
   }
 }
 
-// stored g of one level (global grid, records already holding a / e): per point, the
-// neighbours' coefficients from memory.  In place: g slots are written, a / e only read.
+// stored g of one level (records already holding a / e): per point, the neighbours'
+// coefficients from memory.  In place: g slots are written, a / e only read.  Planes kb +
+// blockIdx.z (global indices, cf at global plane 0; a / e current on planes +-2 around them).
 template <typename T, int DIM, int KIND>
 __global__ void __launch_bounds__(256) build_g_k(T* __restrict__ cf, int nx, int ny, int nz, int rs,
-                                                 Rat<T> rat) {
+                                                 Rat<T> rat, int kb) {
   using L = CoefLayout<DIM, KIND>;
-  const int k = (DIM == 3) ? (int)blockIdx.z : 0;
+  const int k = (DIM == 3) ? kb + (int)blockIdx.z : 0;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nx || j >= ny) return;
@@ -1930,15 +1936,16 @@ __global__ void __launch_bounds__(256) synth_image_k(T* __restrict__ x, Geo g, i
 }
 
 // VED-form tensor T = lp I + (la - lp) v v^T (include/itkVEDMultigridImageFilter.hxx:327-365
-// with V = resp^(1/s), identity where V == 0) on the analytic fields of tests/synth.py
+// with V = resp^(1/s), identity where V == 0) on the analytic fields of tests/synth.py.
+// Global planes kb + blockIdx.z of an nz-plane grid; M at global plane 0, component stride cs.
 __global__ void __launch_bounds__(256) synth_ved_k(double* __restrict__ M, int nx, int ny, int nz,
                                                    uint64_t seed, double eps, double omega,
-                                                   double sens) {
-  const int k = blockIdx.z;
+                                                   double sens, int kb, int64_t cs) {
+  const int k = kb + (int)blockIdx.z;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nx || j >= ny) return;
-  const int64_t n = (int64_t)nx * ny * nz;
+  const int64_t n = cs;
   const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
   const double PI2 = 6.283185307179586;
   const double x = i, y = j, z = k;
@@ -1967,12 +1974,13 @@ __global__ void __launch_bounds__(256) synth_ved_k(double* __restrict__ M, int n
 
 // isotropic c(x) I, c = 1 + 0.5 sin sin sin (period 32)
 __global__ void __launch_bounds__(256) synth_iso_k(double* __restrict__ M, int nx, int ny, int nz,
-                                                   int dim, uint64_t seed) {
-  const int k = blockIdx.z;
+                                                   int dim, uint64_t seed, int kb, int64_t cs) {
+  const int k = kb + (int)blockIdx.z;
   const int j = blockIdx.y * blockDim.y + threadIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nx || j >= ny) return;
-  const int64_t n = (int64_t)nx * ny * nz;
+  const int64_t n = cs;
+  (void)nz;
   const int64_t p = i + (int64_t)nx * (j + (int64_t)ny * k);
   const double PI2 = 6.283185307179586;
   const double ph = 0.3 * (double)seed;

@@ -200,7 +200,14 @@ struct mad_ctx {
   std::vector<LevelGeom> geom;
   int kind = KFULL;
   int ncolors = 4;
-  double* tensor64 = nullptr;  // global SoA fp64 level-0 tensor (device)
+  // level-0 fp64 tensor (SetDiffusionTensor), SoA on the device.  One rank: the whole grid,
+  // component stride N.  Rank slab: per component the slab's planes plus tensor_tg ghost planes
+  // per side (tensor_layout), so no rank ever holds the global tensor; the global planes
+  // [tensor_lo, tensor_hi) inside the grid are the ones set_tensor / synth fill.
+  double* tensor64 = nullptr;
+  int64_t tensor_cs = 0;  // component stride (elements)
+  int tensor_tg = 0;      // ghost planes per side
+  int64_t tensor_lo = 0, tensor_hi = 0;
   bool tensor_set = false;
   bool setup_done = false;
   std::unique_ptr<SolverBase> solver;
@@ -217,6 +224,11 @@ struct mad_ctx {
   Comm comm;
   ~mad_ctx();
 };
+
+// ghost planes per side of a rank's fp64 tensor slab on every distributed level: GHOST
+// coefficient ghost planes, +2 for g's differences of the records (build_g_k), +2 for the
+// tensor differences of the records (build_coef3_k)
+constexpr int TENSOR_GHOST = GHOST + 4;
 
 struct SolverBase {
   virtual ~SolverBase() {}
@@ -1763,144 +1775,167 @@ class Solver final : public SolverBase {
   void convert_in(const void* src, int dt, T* dst, int64_t n) { convert_to(src, dt, dst, n, c_->stream); }
   void convert_out(const T* src, void* dst, int dt, int64_t n) { convert_from(src, dst, dt, n, c_->stream); }
 
-  // GH.hxx:110-201: level-0 DCA from the input tensor, then per level: restrict
-  // every tensor component (coarse centring) and rediscretise.  Done on the full
-  // (global) grid in fp64 on every rank; each rank keeps its slab.
+  // GH.hxx:110-201: level-0 DCA from the input tensor, then per level: restrict every tensor
+  // component (coarse centring) and rediscretise, in fp64.  Rank slabs stay slabs: a
+  // distributed level restricts its own planes from the finer slab (taps past the slab read
+  // the finer level's ghost planes), fills TENSOR_GHOST ghost planes from the neighbours
+  // (Comm::shift_planes, hop by hop where the slab is thinner than that) and builds its
+  // records on the owned + GHOST ghost planes; the first replicated level gathers the last
+  // distributed one (small by construction, plan_geometry).  Per-rank memory O(slab), and the
+  // records are bit-identical to a whole-grid build: global plane indices, the same taps in
+  // the same order.
+  struct TView {
+    double* base;  // component 0, first stored plane
+    int64_t cs;    // component stride
+    int tg;        // ghost planes per side
+    int64_t z0;    // global index of the first owned plane
+    int64_t sz;    // plane size
+    double* at0() const { return base + (tg - z0) * sz; }    // global-plane-indexed
+    double* owned(int k) const { return base + k * cs + tg * sz; }  // component k, plane z0
+  };
+
   void build_operators() {
     const int dim = c_->dim;
     const int ncomp = dim * (dim + 1) / 2;
     const int nl = c_->nlev;
-    double* fine = c_->tensor64;
-    double* own = nullptr;
-    T* full_cf = nullptr;
+    const LevelGeom& G0 = c_->geom[0];
+    TView fine{c_->tensor64, c_->tensor_cs, c_->tensor_tg, G0.z0, G0.n[0] * G0.n[1]};
+    double* own = nullptr;  // the level tensor allocated here (freed once superseded)
     for (int l = 0; l < nl; ++l) {
       const LevelGeom& G = c_->geom[l];
-      const int64_t Ng = G.N;
+      const int64_t sz = G.n[0] * G.n[1];
       if (l > 0) {
         const LevelGeom& Gf = c_->geom[l - 1];
+        const int tgc = G.distributed ? TENSOR_GHOST : 0;
+        const int64_t nzl = G.z1 - G.z0;
+        const int64_t csc = (nzl + 2 * tgc) * sz;
         double* coarse = nullptr;
-        HIP_CHECK(hipMalloc(&coarse, sizeof(double) * Ng * ncomp));
+        HIP_CHECK(hipMalloc(&coarse, sizeof(double) * ncomp * csc));
+        if (tgc) HIP_CHECK(hipMemsetAsync(coarse, 0, sizeof(double) * ncomp * csc, c_->stream));
+        // a replicated level under a distributed one: gather the finer slabs first
+        double* gathered = nullptr;
+        TView src = fine;
+        if (!G.distributed && Gf.distributed) {
+          HIP_CHECK(hipMalloc(&gathered, sizeof(double) * ncomp * Gf.N));
+          for (int k = 0; k < ncomp; ++k)
+            c_->comm.allgather_slabs(fine.owned(k), gathered + k * Gf.N, fine.sz, Gf.n[2], sizeof(double),
+                                     c_->stream);
+          src = TView{gathered, Gf.N, 0, 0, fine.sz};
+        }
+        const bool src_slab = src.tg > 0;
         Geo gf{}, gc{};
-        gf.nx = (int)Gf.n[0]; gf.ny = (int)Gf.n[1]; gf.nz = (int)Gf.n[2];
-        gf.sy = Gf.n[0]; gf.sz = Gf.n[0] * Gf.n[1]; gf.N = Gf.N;
-        gc.nx = (int)G.n[0]; gc.ny = (int)G.n[1]; gc.nz = (int)G.n[2];
-        gc.sy = G.n[0]; gc.sz = G.n[0] * G.n[1]; gc.N = Ng;
-        dim3 gr = grid_for(gc.nx, gc.ny, gc.nz, BLK);
+        gf.nx = (int)Gf.n[0]; gf.ny = (int)Gf.n[1];
+        gf.nz = (int)(src_slab ? Gf.z1 - Gf.z0 : Gf.n[2]);
+        gf.sy = Gf.n[0]; gf.sz = fine.sz; gf.N = gf.sz * gf.nz;
+        gc.nx = (int)G.n[0]; gc.ny = (int)G.n[1]; gc.nz = (int)nzl;
+        gc.zoff = (int)G.z0;
+        gc.sy = G.n[0]; gc.sz = sz; gc.N = sz * nzl;
+        const int fz_shift = src_slab ? (int)Gf.z0 : 0;
         for (int k = 0; k < ncomp; ++k) {
+          const double* fk = src.owned(k);
+          double* ck = coarse + k * csc + tgc * sz;
           if (dim == 3) {
             // z-marching restriction (LDS-staged planes; same taps and fma order as
             // restrict_k, bit-identical), ~1024 blocks
             constexpr int CX = 32, CY = 8;
             const int ntx = (gc.nx + CX - 1) / CX, nty = (gc.ny + CY - 1) / CY;
-            int chunks = std::max(1, std::min((1024 + ntx * nty - 1) / (ntx * nty), gc.nz / 4));
+            int chunks = std::max(1, std::min((1024 + ntx * nty - 1) / (ntx * nty), std::max(1, gc.nz / 4)));
             const int kc = (gc.nz + chunks - 1) / chunks;
             chunks = (gc.nz + kc - 1) / kc;
             hipLaunchKernelGGL((restrict3_k<double, double, CX, CY>),
                                dim3((unsigned)(ntx * nty * chunks)), dim3(CX * CY), 0, c_->stream,
-                               fine + k * Gf.N, gf, coarse + k * Ng, gc, G.cent[0], G.cent[1],
-                               G.cent[2], 0, gc.nz, kc, ntx);
-          } else
-            hipLaunchKernelGGL((restrict_k<double, double, 2>), gr, BLK, 0, c_->stream,
-                               fine + k * Gf.N, gf, coarse + k * Ng, gc, G.cent[0], G.cent[1],
-                               G.cent[2], 0);
+                               fk, gf, ck, gc, G.cent[0], G.cent[1], G.cent[2], fz_shift,
+                               (int)G.n[2], kc, ntx);
+          } else {
+            dim3 gr = grid_for(gc.nx, gc.ny, gc.nz, BLK);
+            hipLaunchKernelGGL((restrict_k<double, double, 2>), gr, BLK, 0, c_->stream, fk, gf, ck, gc,
+                               G.cent[0], G.cent[1], G.cent[2], 0);
+          }
+          HIP_CHECK(hipGetLastError());
+          // the coarse slab's ghost planes, hop by hop (a hop moves at most one slab depth)
+          for (int D = 0; D < tgc;) {
+            const int d = (int)std::min<int64_t>(nzl, tgc - D);
+            c_->comm.shift_planes(ck, sz, (int)nzl, D, d, G.z0 > 0, G.z1 < G.n[2], sizeof(double), true,
+                                  c_->stream);
+            D += d;
+          }
         }
-        HIP_CHECK(hipGetLastError());
-        if (own) {
-          HIP_CHECK(hipStreamSynchronize(c_->stream));
-          HIP_CHECK(hipFree(own));
-        }
+        HIP_CHECK(hipStreamSynchronize(c_->stream));
+        if (gathered) HIP_CHECK(hipFree(gathered));
+        if (own) HIP_CHECK(hipFree(own));
         own = coarse;
-        fine = coarse;
+        fine = TView{coarse, csc, tgc, G.z0, sz};
       }
       LevelData<T>& L = lv_[l];
-      const bool slab = (L.g.N != Ng);
-      T* dst = L.cf;
-      if (slab) {
-        HIP_CHECK(hipMalloc(&full_cf, sizeof(T) * Ng * L.g.rs));
-        dst = full_cf;
-      }
-      dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
-      if (dim == 3) {
-        // z-marching (build_coef3_k): chunks of planes sized for ~4096 blocks of 64 x 4
+      // records on planes [g0, g1) (owned + GHOST ghost planes on a slab); their a / e on
+      // [w0, w1) (g's differences reach two planes further)
+      const bool dist = G.distributed;
+      const int64_t g0 = dist ? std::max<int64_t>(G.z0 - GHOST, 0) : 0;
+      const int64_t g1 = dist ? std::min<int64_t>(G.z1 + GHOST, G.n[2]) : G.n[2];
+      const int64_t w0 = dist ? std::max<int64_t>(g0 - 2, 0) : 0;
+      const int64_t w1 = dist ? std::min<int64_t>(g1 + 2, G.n[2]) : G.n[2];
+      const int64_t cplane = sz * L.g.rs;
+      T* win = nullptr;  // slab: the records of [w0, w1); whole grid: L.cf itself
+      if (dist) HIP_CHECK(hipMalloc(&win, sizeof(T) * (w1 - w0) * cplane));
+      T* rec0 = dist ? win - w0 * cplane : L.cf;  // global-plane-indexed records
+      const CoefFactors cfac = coef_factors(G.h, c_->d.time_step);
+      // z-marching (build_coef3_k): chunks of planes sized for ~4096 blocks of 64 x 4
+      auto coef3 = [&](auto* out, int rs, int64_t kb, int64_t ke) {
+        using U = std::remove_pointer_t<decltype(out)>;
         const int bx = ((int)G.n[0] + 63) / 64, by = ((int)G.n[1] + 3) / 4;
-        const int nzg = (int)G.n[2];
-        int chunks = std::max(1, std::min(nzg, (4096 + bx * by - 1) / (bx * by)));
-        const int kc = (nzg + chunks - 1) / chunks;
-        chunks = (nzg + kc - 1) / kc;
+        const int nzw = (int)(ke - kb);
+        int chunks = std::max(1, std::min(nzw, (4096 + bx * by - 1) / (bx * by)));
+        const int kc = (nzw + chunks - 1) / chunks;
+        chunks = (nzw + kc - 1) / kc;
         auto go = [&](auto K) {
-          hipLaunchKernelGGL((build_coef3_k<T, decltype(K)::value>), dim3(bx, by, chunks), BLK, 0,
-                             c_->stream, fine, (int)G.n[0], (int)G.n[1], nzg,
-                             coef_factors(G.h, c_->d.time_step), dst, L.g.rs, kc);
+          hipLaunchKernelGGL((build_coef3_k<U, decltype(K)::value>), dim3(bx, by, chunks), BLK, 0,
+                             c_->stream, fine.at0(), (int)G.n[0], (int)G.n[1], (int)G.n[2], cfac, out, rs,
+                             kc, (int)kb, (int)ke, fine.cs);
         };
         if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
         else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
         else go(std::integral_constant<int, KISO>{});
+      };
+      if (dim == 3) {
+        coef3(rec0, L.g.rs, w0, w1);
       } else {
+        dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
         dispatch(dim, c_->kind, [&](auto D, auto K) {
-          hipLaunchKernelGGL((build_coef_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
-                             (int)G.n[0], (int)G.n[1], (int)G.n[2],
-                             coef_factors(G.h, c_->d.time_step), dst, L.g.rs);
+          hipLaunchKernelGGL((build_coef_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, fine.base,
+                             (int)G.n[0], (int)G.n[1], (int)G.n[2], cfac, rec0, L.g.rs);
         });
       }
       HIP_CHECK(hipGetLastError());
-      // g from the stored a / e (build_g_k): the one definition every kernel shares,
-      // including the sweeps that recompute g in-kernel instead of reading it
-      dispatch(dim, c_->kind, [&](auto D, auto K) {
-        hipLaunchKernelGGL((build_g_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, dst,
-                           (int)G.n[0], (int)G.n[1], (int)G.n[2], L.g.rs, L.rat);
-      });
-      HIP_CHECK(hipGetLastError());
-      if (slab) {
-        // owned planes plus up to GHOST neighbour planes on each side (whole plane blocks)
-        const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
-        const int64_t p1 = std::min<int64_t>(G.z1 + GHOST, G.n[2]);
-        const int64_t cplane = L.g.sz * L.g.rs;
-        HIP_CHECK(hipMemcpyAsync(L.cf + (p0 - G.z0) * cplane, full_cf + p0 * cplane,
-                                 sizeof(T) * (p1 - p0) * cplane, hipMemcpyDeviceToDevice,
-                                 c_->stream));
+      // g from the stored a / e (build_g_k): the one definition every kernel shares
+      {
+        dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)(g1 - g0), BLK);
+        dispatch(dim, c_->kind, [&](auto D, auto K) {
+          hipLaunchKernelGGL((build_g_k<T, D.value, K.value>), gr, BLK, 0, c_->stream, rec0,
+                             (int)G.n[0], (int)G.n[1], (int)G.n[2], L.g.rs, L.rat, (int)g0);
+        });
+        HIP_CHECK(hipGetLastError());
+      }
+      if (dist) {
+        HIP_CHECK(hipMemcpyAsync(L.cf + (g0 - G.z0) * cplane, win + (g0 - w0) * cplane,
+                                 sizeof(T) * (g1 - g0) * cplane, hipMemcpyDeviceToDevice, c_->stream));
         HIP_CHECK(hipStreamSynchronize(c_->stream));
-        HIP_CHECK(hipFree(full_cf));
-        full_cf = nullptr;
+        HIP_CHECK(hipFree(win));
       }
       if (l == 0 && refine_) {
         // the refined system's operator: fp64 records, g from the fp64 tensor (build_coef*_k
         // restate GH.hxx:298-516 directly; no build_g_k pass), owned + ghost planes
-        double* full64 = cf64_;
-        if (slab) HIP_CHECK(hipMalloc(&full64, sizeof(double) * Ng * ncoef_));
         if (dim == 3) {
-          const int bx = ((int)G.n[0] + 63) / 64, by = ((int)G.n[1] + 3) / 4;
-          const int nzg = (int)G.n[2];
-          int chunks = std::max(1, std::min(nzg, (4096 + bx * by - 1) / (bx * by)));
-          const int kc = (nzg + chunks - 1) / chunks;
-          chunks = (nzg + kc - 1) / kc;
-          auto go = [&](auto K) {
-            hipLaunchKernelGGL((build_coef3_k<double, decltype(K)::value>), dim3(bx, by, chunks), BLK, 0,
-                               c_->stream, fine, (int)G.n[0], (int)G.n[1], nzg,
-                               coef_factors(G.h, c_->d.time_step), full64, ncoef_, kc);
-          };
-          if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
-          else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
-          else go(std::integral_constant<int, KISO>{});
+          coef3(cf64_ - G.z0 * sz * ncoef_, ncoef_, g0, g1);
         } else {
+          dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
           dispatch(dim, c_->kind, [&](auto D, auto K) {
-            hipLaunchKernelGGL((build_coef_k<double, D.value, K.value>), gr, BLK, 0, c_->stream, fine,
-                               (int)G.n[0], (int)G.n[1], (int)G.n[2],
-                               coef_factors(G.h, c_->d.time_step), full64, ncoef_);
+            hipLaunchKernelGGL((build_coef_k<double, D.value, K.value>), gr, BLK, 0, c_->stream, fine.base,
+                               (int)G.n[0], (int)G.n[1], (int)G.n[2], cfac, cf64_, ncoef_);
           });
         }
         HIP_CHECK(hipGetLastError());
-        if (slab) {
-          const int64_t p0 = std::max<int64_t>(G.z0 - GHOST, 0);
-          const int64_t p1 = std::min<int64_t>(G.z1 + GHOST, G.n[2]);
-          const int64_t cplane = L.g.sz * ncoef_;
-          HIP_CHECK(hipMemcpyAsync(cf64_ + (p0 - G.z0) * cplane, full64 + p0 * cplane,
-                                   sizeof(double) * (p1 - p0) * cplane, hipMemcpyDeviceToDevice,
-                                   c_->stream));
-          HIP_CHECK(hipStreamSynchronize(c_->stream));
-          HIP_CHECK(hipFree(full64));
-        }
       }
-      if (l == nl - 1) build_coarsest_matrix(fine);
+      if (l == nl - 1) build_coarsest_matrix(fine.base);  // replicated: the whole grid
     }
     HIP_CHECK(hipStreamSynchronize(c_->stream));
     if (own) HIP_CHECK(hipFree(own));
@@ -2105,6 +2140,21 @@ int guarded(mad_ctx* c, F&& f) {
 
 void use_device(mad_ctx* c) { HIP_CHECK(hipSetDevice(c->device)); }
 
+// the level-0 tensor indexed by global point: component c of global point p at [c * tensor_cs + p]
+// (valid for the planes the slab stores)
+double* tensor_at0(const mad_ctx* c) {
+  const LevelGeom& G = c->geom[0];
+  return c->tensor64 + (c->tensor_tg - G.z0) * G.n[0] * G.n[1];
+}
+
+void tensor_alloc(mad_ctx* c) {
+  if (c->tensor64) return;
+  const int ncomp = c->dim * (c->dim + 1) / 2;
+  HIP_CHECK(hipMalloc(&c->tensor64, sizeof(double) * ncomp * c->tensor_cs));
+  // ghost planes outside the grid stay zero (never read)
+  if (c->tensor_tg) HIP_CHECK(hipMemsetAsync(c->tensor64, 0, sizeof(double) * ncomp * c->tensor_cs, c->stream));
+}
+
 std::vector<LevelGeom> plan_geometry(const mad_desc& d) {
   const int dim = d.dim;
   int64_t n0[3] = {d.size[0], d.size[1], dim == 3 ? d.size[2] : 1};
@@ -2164,6 +2214,11 @@ std::vector<LevelGeom> plan_geometry(const mad_desc& d) {
 void compute_geometry(mad_ctx* c) {
   c->geom = plan_geometry(c->d);
   c->nlev = (int)c->geom.size();
+  const LevelGeom& G = c->geom[0];
+  c->tensor_tg = G.distributed ? TENSOR_GHOST : 0;
+  c->tensor_cs = (G.z1 - G.z0 + 2 * c->tensor_tg) * G.n[0] * G.n[1];
+  c->tensor_lo = std::max<int64_t>(G.z0 - c->tensor_tg, 0);
+  c->tensor_hi = std::min<int64_t>(G.z1 + c->tensor_tg, G.n[2]);
 }
 
 }  // namespace
@@ -2269,30 +2324,39 @@ int mad_get_desc(const mad_ctx* c, mad_desc* out) {
   return MAD_OK;
 }
 
-static int set_tensor_impl(mad_ctx* c, const void* p, int32_t dtype, bool dev) {
+// p: AoS tensor of global planes [first, ...) covering the planes this context stores
+// ([tensor_lo, tensor_hi): the whole grid on one rank, the slab and its ghost planes on a rank)
+static int set_tensor_impl(mad_ctx* c, const void* p, int32_t dtype, bool dev, int64_t first,
+                           int64_t nplanes) {
   if (!c) return MAD_ERR_INVALID;
   return guarded(c, [&] {
     REQUIRE(p, MAD_ERR_INVALID, "null tensor");
     REQUIRE(dtype == MAD_F32 || dtype == MAD_F64, MAD_ERR_INVALID, "tensor dtype must be F32/F64");
+    REQUIRE(first <= c->tensor_lo && first + nplanes >= c->tensor_hi, MAD_ERR_INVALID,
+            "tensor planes [" + std::to_string(first) + ", " + std::to_string(first + nplanes) +
+                ") do not cover [" + std::to_string(c->tensor_lo) + ", " + std::to_string(c->tensor_hi) +
+                ") (mad_tensor_planes)");
     use_device(c);
     const LevelGeom& G = c->geom[0];
     const int ncomp = c->dim * (c->dim + 1) / 2;
-    const int64_t n = G.N;
-    if (!c->tensor64) HIP_CHECK(hipMalloc(&c->tensor64, sizeof(double) * n * ncomp));
+    const int64_t sz = G.n[0] * G.n[1];
+    const int64_t n = (c->tensor_hi - c->tensor_lo) * sz;  // points this context stores
+    tensor_alloc(c);
     const size_t bytes = dtype_size(dtype) * n * ncomp;
-    const void* src = p;
+    const void* src = (const char*)p + dtype_size(dtype) * (c->tensor_lo - first) * sz * ncomp;
     void* stage = nullptr;
     if (!dev) {
       HIP_CHECK(hipMalloc(&stage, bytes));
-      HIP_CHECK(hipMemcpyAsync(stage, p, bytes, hipMemcpyHostToDevice, c->stream));
+      HIP_CHECK(hipMemcpyAsync(stage, src, bytes, hipMemcpyHostToDevice, c->stream));
       src = stage;
     }
+    double* dst = tensor_at0(c) + c->tensor_lo * sz;
     if (dtype == MAD_F64)
       hipLaunchKernelGGL((aos_to_soa_k<double>), dim3(flat_blocks(n)), dim3(256), 0, c->stream,
-                         (const double*)src, c->tensor64, n, ncomp);
+                         (const double*)src, dst, n, ncomp, c->tensor_cs);
     else
       hipLaunchKernelGGL((aos_to_soa_k<float>), dim3(flat_blocks(n)), dim3(256), 0, c->stream,
-                         (const float*)src, c->tensor64, n, ncomp);
+                         (const float*)src, dst, n, ncomp, c->tensor_cs);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(c->stream));
     if (stage) HIP_CHECK(hipFree(stage));
@@ -2302,11 +2366,23 @@ static int set_tensor_impl(mad_ctx* c, const void* p, int32_t dtype, bool dev) {
 }
 
 int mad_set_tensor(mad_ctx* c, const void* host_aos, int32_t dtype) {
-  return set_tensor_impl(c, host_aos, dtype, false);
+  return c ? set_tensor_impl(c, host_aos, dtype, false, 0, c->geom[0].n[2]) : MAD_ERR_INVALID;
 }
 
 int mad_set_tensor_device(mad_ctx* c, const void* dev_aos, int32_t dtype) {
-  return set_tensor_impl(c, dev_aos, dtype, true);
+  return c ? set_tensor_impl(c, dev_aos, dtype, true, 0, c->geom[0].n[2]) : MAD_ERR_INVALID;
+}
+
+int mad_set_tensor_planes(mad_ctx* c, const void* host_aos, int32_t dtype, int64_t first_plane,
+                          int64_t nplanes) {
+  return c ? set_tensor_impl(c, host_aos, dtype, false, first_plane, nplanes) : MAD_ERR_INVALID;
+}
+
+int mad_tensor_planes(const mad_ctx* c, int64_t* first_plane, int64_t* nplanes) {
+  if (!c || !first_plane || !nplanes) return MAD_ERR_INVALID;
+  *first_plane = c->tensor_lo;
+  *nplanes = c->tensor_hi - c->tensor_lo;
+  return MAD_OK;
 }
 
 int mad_bench_synth_tensor(mad_ctx* c, int32_t kind, uint64_t seed) {
@@ -2314,16 +2390,16 @@ int mad_bench_synth_tensor(mad_ctx* c, int32_t kind, uint64_t seed) {
   return guarded(c, [&] {
     use_device(c);
     const LevelGeom& G = c->geom[0];
-    const int ncomp = c->dim * (c->dim + 1) / 2;
-    if (!c->tensor64) HIP_CHECK(hipMalloc(&c->tensor64, sizeof(double) * G.N * ncomp));
-    dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
+    tensor_alloc(c);
+    const int kb = (int)c->tensor_lo;
+    dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)(c->tensor_hi - c->tensor_lo), BLK);
     if (kind == 0) {
       REQUIRE(c->dim == 3, MAD_ERR_INVALID, "VED-form synthetic tensor is 3D");
-      hipLaunchKernelGGL(synth_ved_k, gr, BLK, 0, c->stream, c->tensor64, (int)G.n[0],
-                         (int)G.n[1], (int)G.n[2], seed, 0.01, 1.5, 10.0);
+      hipLaunchKernelGGL(synth_ved_k, gr, BLK, 0, c->stream, tensor_at0(c), (int)G.n[0],
+                         (int)G.n[1], (int)G.n[2], seed, 0.01, 1.5, 10.0, kb, c->tensor_cs);
     } else if (kind == 1) {
-      hipLaunchKernelGGL(synth_iso_k, gr, BLK, 0, c->stream, c->tensor64, (int)G.n[0],
-                         (int)G.n[1], (int)G.n[2], c->dim, seed);
+      hipLaunchKernelGGL(synth_iso_k, gr, BLK, 0, c->stream, tensor_at0(c), (int)G.n[0],
+                         (int)G.n[1], (int)G.n[2], c->dim, seed, kb, c->tensor_cs);
     } else {
       throw MadError(MAD_ERR_INVALID, "unknown synthetic tensor kind");
     }
@@ -2337,24 +2413,33 @@ int mad_bench_synth_tensor(mad_ctx* c, int32_t kind, uint64_t seed) {
 static void setup_impl(mad_ctx* c) {
   REQUIRE(c->tensor_set, MAD_ERR_STATE, "SetDiffusionTensor (mad_set_tensor) must come first");
   use_device(c);
+  REQUIRE(c->d.nranks == 1 || c->comm.active(), MAD_ERR_STATE,
+          "nranks > 1: join the communicator (mad_comm_init*) before mad_setup (the operator "
+          "build exchanges tensor ghost planes)");
   auto t0 = std::chrono::steady_clock::now();
   const LevelGeom& G = c->geom[0];
-  const int ncomp = c->dim * (c->dim + 1) / 2;
-  (void)ncomp;
-  // resolve the tensor kind, and reject a non-finite tensor (it would surface later as
-  // a singular coarsest operator or a NaN image)
+  // resolve the tensor kind (over all ranks: every slab must build the same kind of operator),
+  // and reject a non-finite tensor (it would surface later as a singular coarsest operator or
+  // a NaN image)
   int kind = KFULL;
   {
+    const int64_t sz = G.n[0] * G.n[1];
+    const int64_t n = (G.z1 - G.z0) * sz;  // owned points
     unsigned int* flags = nullptr;
     HIP_CHECK(hipMalloc(&flags, sizeof(unsigned int) * 3));
     HIP_CHECK(hipMemsetAsync(flags, 0, sizeof(unsigned int) * 3, c->stream));
-    hipLaunchKernelGGL(tensor_kind_k, dim3(flat_blocks(G.N, 2048)), dim3(256), 0, c->stream,
-                       c->tensor64, G.N, c->dim, flags);
+    hipLaunchKernelGGL(tensor_kind_k, dim3(flat_blocks(n, 2048)), dim3(256), 0, c->stream,
+                       tensor_at0(c) + G.z0 * sz, n, c->tensor_cs, c->dim, flags);
     HIP_CHECK(hipGetLastError());
     unsigned int hf[3];
     HIP_CHECK(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     HIP_CHECK(hipFree(flags));
+    if (c->comm.active()) {
+      double v[3] = {(double)hf[0], (double)hf[1], (double)hf[2]};
+      c->comm.allreduce_host(v, 3, 1, c->stream);
+      for (int q = 0; q < 3; ++q) hf[q] = v[q] != 0.0;
+    }
     REQUIRE(hf[2] == 0, MAD_ERR_NUMERIC, "diffusion tensor has non-finite (NaN / Inf) entries");
     if (c->d.tensor_kind == MAD_TENSOR_AUTO) kind = hf[0] ? KFULL : (hf[1] ? KDIAG : KISO);
     else kind = c->d.tensor_kind;  // MAD_TENSOR_* == KISO/KDIAG/KFULL
@@ -2367,14 +2452,6 @@ static void setup_impl(mad_ctx* c) {
   }
   c->solver->setup(c);
   c->setup_done = true;
-  if (c->d.nranks > 1) {
-    // a rank slab's setup works on the global fp64 tensor (replicated operator build);
-    // once the slab's operators exist it is dead weight (26 GB at 1024 x 1024 x 512), so
-    // it is released -- the next setup needs a new mad_set_tensor, as after construction
-    HIP_CHECK(hipFree(c->tensor64));
-    c->tensor64 = nullptr;
-    c->tensor_set = false;
-  }
   c->setup_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }

@@ -403,9 +403,12 @@ void ved_tensor_impl(mad_ved_ctx* v) {
   if (!v->resp) HIP_CHECK(hipMalloc(&v->resp, sizeof(double) * N));
   if (!v->dir) HIP_CHECK(hipMalloc(&v->dir, sizeof(double) * 3 * N));
   for (int s = 0; s < v->d.nscales; ++s) ved_scale<T>(v, v->d.scales[s], VED_UPDATE, s == 0, nullptr);
-  if (!c->tensor64) HIP_CHECK(hipMalloc(&c->tensor64, sizeof(double) * 6 * N));
-  hipLaunchKernelGGL(ved_tensor_k, dim3(flat_blocks(N)), dim3(256), 0, c->stream, v->resp, v->dir,
-                     c->tensor64, N, v->d.epsilon, v->d.omega, v->d.sensitivity);
+  // the tensor planes this rank's solver stores (its slab + ghost planes; all on one GPU)
+  tensor_alloc(c);
+  const int64_t sz = v->n[0] * v->n[1];
+  const int64_t q0 = c->tensor_lo * sz, q1 = c->tensor_hi * sz;
+  hipLaunchKernelGGL(ved_tensor_k, dim3(flat_blocks(q1 - q0)), dim3(256), 0, c->stream, v->resp, v->dir,
+                     tensor_at0(c), N, q0, q1, c->tensor_cs, v->d.epsilon, v->d.omega, v->d.sensitivity);
   HIP_CHECK(hipGetLastError());
   c->tensor_set = true;
   c->setup_done = false;  // DiffusionStep builds a new filter per iteration (VED.hxx:386)
@@ -614,6 +617,7 @@ int mad_ved_tensor(mad_ved_ctx* v, const void* image, int32_t dtype, double* ten
                    double* response) {
   if (!v || !image || !tensor_soa) return MAD_ERR_INVALID;
   return ved_guarded(v, [&] {
+    REQUIRE(v->mad->d.nranks == 1, MAD_ERR_UNSUPPORTED, "mad_ved_tensor returns the whole grid: one rank only");
     HIP_CHECK(hipSetDevice(v->mad->device));
     ved_load_image(v, image, dtype, false);
     ved_tensor_any(v);

@@ -859,9 +859,12 @@ __global__ void __launch_bounds__(256) ved_hess_k(const S* __restrict__ H, int64
 // i.e. T = a I + (c - a) v v^T with v the third column; identity elsewhere.
 __global__ void __launch_bounds__(256) ved_tensor_k(const double* __restrict__ resp,
                                                     const double* __restrict__ dir,
-                                                    double* __restrict__ T, int64_t n, double eps,
+                                                    double* __restrict__ T, int64_t n, int64_t q0,
+                                                    int64_t q1, int64_t cs, double eps,
                                                     double omega, double sens) {
-  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+  // points [q0, q1) of the n-point grid (a rank slab's tensor planes); T at global point 0 with
+  // component stride cs (= n on one GPU)
+  for (int64_t q = q0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < q1;
        q += (int64_t)gridDim.x * blockDim.x) {
     const double V = pow(resp[q], 1. / sens);
     if (V > 0) {
@@ -870,18 +873,18 @@ __global__ void __launch_bounds__(256) ved_tensor_k(const double* __restrict__ r
       const double d = c - a;
       const double v0 = dir[q], v1 = dir[n + q], v2 = dir[2 * n + q];
       T[q] = a + d * v0 * v0;
-      T[n + q] = d * v0 * v1;
-      T[2 * n + q] = d * v0 * v2;
-      T[3 * n + q] = a + d * v1 * v1;
-      T[4 * n + q] = d * v1 * v2;
-      T[5 * n + q] = a + d * v2 * v2;
+      T[cs + q] = d * v0 * v1;
+      T[2 * cs + q] = d * v0 * v2;
+      T[3 * cs + q] = a + d * v1 * v1;
+      T[4 * cs + q] = d * v1 * v2;
+      T[5 * cs + q] = a + d * v2 * v2;
     } else {
       T[q] = 1.;
-      T[n + q] = 0.;
-      T[2 * n + q] = 0.;
-      T[3 * n + q] = 1.;
-      T[4 * n + q] = 0.;
-      T[5 * n + q] = 1.;
+      T[cs + q] = 0.;
+      T[2 * cs + q] = 0.;
+      T[3 * cs + q] = 1.;
+      T[4 * cs + q] = 0.;
+      T[5 * cs + q] = 1.;
     }
   }
 }

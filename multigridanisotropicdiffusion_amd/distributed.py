@@ -58,7 +58,14 @@ def slabs(global_shape, nranks):
 
 
 def _rdzv_path(tag):
-    key = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}-{tag}"
+    """The id file of one communicator: keyed by the launcher shared by all ranks (parent
+    pid), MASTER_PORT and, under torchrun, the elastic run id and restart count (so a
+    restarted job never reads the id a dead rank 0 left behind)."""
+    parts = [str(os.getppid()), os.environ.get("MASTER_PORT", "0")]
+    for k in ("TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT"):
+        if os.environ.get(k):
+            parts.append(os.environ[k])
+    key = "-".join(parts + [str(tag)])
     return os.path.join(tempfile.gettempdir(), f"mad_rccl_uid_{key}")
 
 
@@ -69,6 +76,13 @@ def bootstrap_node(solver, rank, world, tag="0", timeout=120.0):
     the 128-byte unique id atomically (tmp file + rename); the others poll for it.
     ncclCommInitRank is collective, so once it returns on rank 0 every rank has
     read the id and rank 0 removes the file."""
+    if world > 1 and not os.environ.get("MASTER_PORT"):
+        # every rank must derive the same key; without the launcher's MASTER_PORT two
+        # concurrent jobs under one parent could meet in the same file
+        raise RuntimeError("bootstrap_node: MASTER_PORT is not set; launch the ranks with "
+                           "torch.distributed.run (or export MASTER_PORT, identical on every rank)")
+    if not 0 <= rank < world:
+        raise ValueError(f"bootstrap_node: rank {rank} outside world {world}")
     path = _rdzv_path(tag)
     if rank == 0:
         uid = comm_unique_id()

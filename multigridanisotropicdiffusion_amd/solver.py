@@ -117,6 +117,25 @@ class Solver:
         self._check(self._L.mad_set_tensor(self._ctx, t.ctypes.data_as(ctypes.c_void_p),
                                            C.F64 if t.dtype == np.float64 else C.F32))
 
+    def tensor_planes(self):
+        """Global z planes [first, first + n) of the tensor this context stores
+        (mad_tensor_planes): the whole grid on one rank, slab + ghost planes on a rank."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._L.mad_tensor_planes(self._ctx, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, a.value + b.value
+
+    def set_tensor_planes(self, tensor, first_plane):
+        """SetDiffusionTensor from global planes [first_plane, ...) only (AoS (z, y, x, ncomp)
+        or SoA (ncomp, z, y, x) of those planes; mad_set_tensor_planes)."""
+        nc = self.dim * (self.dim + 1) // 2
+        t = np.asarray(tensor)
+        if t.shape[0] == nc and t.ndim == self.dim + 1 and t.shape[-1] != nc:
+            t = np.moveaxis(t, 0, -1)
+        t = np.ascontiguousarray(t, dtype=np.float64 if t.dtype == np.float64 else np.float32)
+        self._check(self._L.mad_set_tensor_planes(self._ctx, t.ctypes.data_as(ctypes.c_void_p),
+                                                  C.F64 if t.dtype == np.float64 else C.F32,
+                                                  int(first_plane), int(t.shape[0])))
+
     def synth_tensor(self, kind=0, seed=4):
         self._check(self._L.mad_bench_synth_tensor(self._ctx, kind, seed))
 

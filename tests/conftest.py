@@ -1,5 +1,9 @@
 import os
+import signal
+import socket
+import subprocess
 import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -15,6 +19,102 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP library)")
     config.addinivalue_line("markers", "slow: longer GPU cases")
+
+
+# ---------------------------------------------------------------- multi-process RCCL job
+# tests/test_gpu_multiproc.py compares N RCCL rank processes with the LOCAL transport.  The
+# rank processes must start before this process makes any GPU call, so they are launched at
+# session start (when the gpu tests are selected and >= 2 GPUs are visible) and joined by the
+# test.  GPUs are counted in a child process: this one must not initialise HIP first.
+
+_MP = {}
+
+
+def _gpu_selected(config):
+    m = config.getoption("markexpr", "") or ""
+    return "gpu" in m and "not gpu" not in m
+
+
+def _count_gpus():
+    code = ("import ctypes\n"
+            "for n in ('libamdhip64.so', '/opt/rocm/lib/libamdhip64.so'):\n"
+            "    try:\n        L = ctypes.CDLL(n); break\n"
+            "    except OSError:\n        L = None\n"
+            "c = ctypes.c_int(0)\n"
+            "print(c.value if L is not None and L.hipGetDeviceCount(ctypes.byref(c)) == 0 else 0)\n")
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else 0
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def pytest_sessionstart(session):
+    config = session.config
+    if not _gpu_selected(config) or os.environ.get("MAD_SKIP_MULTIPROC"):
+        return
+    world = min(_count_gpus(), 8)
+    if world < 2:
+        return
+    outdir = tempfile.mkdtemp(prefix="mad_mp_")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               WORLD_SIZE=str(world))
+    env.setdefault("NCCL_SOCKET_IFNAME", "lo")  # one node: bootstrap on loopback
+    procs, logs = [], []
+    for r in range(world):
+        log = os.path.join(outdir, f"rank{r}.log")
+        with open(log, "w") as f:
+            procs.append(subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "tests", "mp_rank.py"), outdir],
+                env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=f, stderr=subprocess.STDOUT,
+                cwd=ROOT, start_new_session=True))
+        logs.append(log)
+    _MP["job"] = dict(procs=procs, logs=logs, outdir=outdir, world=world)
+
+
+def multiproc_job(config):
+    return _MP.get("job")
+
+
+def join_multiproc(job, timeout):
+    """Exit codes of the rank processes; kills the whole job (every process group) when one
+    fails or the time runs out, so no rank is left waiting in a collective."""
+    import time
+    t_end = time.monotonic() + timeout
+    procs = job["procs"]
+    while time.monotonic() < t_end:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs) or any(rc not in (None, 0) for rc in rcs):
+            break
+        time.sleep(0.5)
+    _kill_job(job)
+    return [p.poll() if p.poll() is not None else -9 for p in procs]
+
+
+def _kill_job(job):
+    for p in job["procs"]:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+    for p in job["procs"]:
+        try:
+            p.wait(30)
+        except subprocess.TimeoutExpired:
+            pass
+
+
+def pytest_sessionfinish(session, exitstatus):
+    job = _MP.pop("job", None)
+    if job is not None:
+        _kill_job(job)
 
 
 @pytest.fixture(scope="session")

@@ -62,6 +62,48 @@ def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle):
         assert abs(o[2] - ref[2]) <= 1e-12 * ref[2]
 
 
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_slab_tensor_setup_is_bitwise(nranks):
+    """Each rank sets only the tensor planes it stores (mad_tensor_planes: its slab + 8 ghost
+    planes per side) and builds its operators from them, coarse tensor ghost planes exchanged
+    hop by hop (8 ranks: 8-plane level-0 slabs, 2-plane level-2 slabs, so ghost regions span
+    four neighbours).  Sweeps and V-cycles equal the single-rank run bit for bit; a second
+    set_tensor + setup on the same contexts (the next VED iteration's pattern) too."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (64, 40, 36)
+    T = synth.random_spd(shape, seed=11)  # (6, z, y, x)
+    x = synth.image(shape, seed=12)
+    b = synth.image(shape, seed=13)
+    sl = D.slabs(shape, nranks)
+
+    def fn(r, s):
+        z0, z1 = (0, shape[0]) if r is None else sl[r]
+        out = []
+        for scale in (1.0, 1.75):  # two setups on one context
+            Ts = T * scale
+            if r is None:
+                s.set_tensor(Ts)
+            else:
+                lo, hi = s.tensor_planes()
+                assert lo == max(z0 - 8, 0) and hi == min(z1 + 8, shape[0])
+                s.set_tensor_planes(Ts[:, lo:hi], lo)
+            s.setup()
+            s.upload(0, M.capi.X, x[z0:z1])
+            s.upload(0, M.capi.B, b[z0:z1])
+            s.smooth(0, 3)
+            s.vcycle()
+            out.append(s.download(0, M.capi.X))
+        return out
+
+    s = M.Solver(shape, time_step=0.4)
+    ref = fn(None, s)
+    s.close()
+    out = D.run_local(nranks, fn, shape, time_step=0.4)
+    for q in range(2):
+        np.testing.assert_array_equal(np.concatenate([o[q] for o in out]), ref[q])
+
+
 @pytest.mark.parametrize("nranks", [2, 4])
 def test_distributed_filter_run_matches_single(nranks):
     """mad_run on slabs (each rank passes its own slab of the image)."""
@@ -166,3 +208,40 @@ def test_solo_transport_times_one_rank():
             assert s.bench_vcycle(3) > 0
         assert np.isfinite(s.download(0, M.capi.X)).all()
         s.close()
+
+
+@pytest.mark.parametrize("cycle", [0, 2])
+def test_solo_graph_replayed_vcycle_equals_eager(cycle):
+    """The multi-rank V-cycle replays a captured hipGraph on RCCL / SOLO ranks (host bookkeeping
+    of which ghost planes are current decides what the graph re-exchanges).  On the SOLO
+    transport (deterministic: every exchange a device copy) the same sequence -- sweeps,
+    several V-cycles, an odd sweep count in between (the ping-pong parity flips), more
+    V-cycles -- equals the eager execution (mad_desc.options MAD_OPT_EAGER_RANK_VCYCLE) bit for
+    bit on every level's x and b."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (128, 64, 64)
+    z0, z1 = D.slabs(shape, 4)[2]
+    out = {}
+    for opt in (0, M.capi.OPT_EAGER_RANK_VCYCLE):
+        s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
+                     global_shape=shape, options=opt)
+        s.comm_init_solo()
+        s.synth_tensor(kind=0, seed=9)
+        s.setup()
+        s.synth_level(0, M.capi.B, 3)
+        s.synth_level(0, M.capi.X, 4)
+        s.smooth(0, 2)
+        for _ in range(3):
+            s.vcycle()
+        s.smooth(0, 1)
+        for _ in range(2):
+            s.vcycle()
+        out[opt] = [(s.download(l, M.capi.X), s.download(l, M.capi.B))
+                    for l in range(s.num_levels)]
+        s.close()
+    a, b = out[0], out[M.capi.OPT_EAGER_RANK_VCYCLE]
+    for l, ((xa, ba), (xb, bb)) in enumerate(zip(a, b)):
+        assert np.isfinite(xa).all()
+        np.testing.assert_array_equal(xa, xb, err_msg=f"x, level {l}")
+        np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")

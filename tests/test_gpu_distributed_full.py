@@ -8,12 +8,10 @@ BIT for bit, with the default (fused, boundary + interior overlapped) sweep on t
 global coordinates (mad_bench_synth_tensor / mad_bench_synth_level), so every rank
 builds the same operator the single-rank run builds.
 
-Memory: a rank slab's setup works on the global fp64 tensor (26 GB at C5) and
-releases it afterwards (mad_setup, nranks > 1); the rank setups are serialised
-here so that only one global tensor is alive at a time on the shared device.
+Memory: a rank builds its operators from its own tensor slab (+ TENSOR_GHOST ghost planes
+exchanged level by level; mad_setup is collective), so the ranks' setups run concurrently
+and no global fp64 tensor (26 GB at C5) exists anywhere.
 """
-import threading
-
 import numpy as np
 import pytest
 
@@ -49,12 +47,12 @@ def test_full_size_slabs_bitwise(gshape, nranks, cycle):
     nlev = s.num_levels
     s.close()
 
-    lock = threading.Lock()
-
     def body(r, s):
-        with lock:  # one global fp64 tensor alive at a time on the shared GPU
-            s.synth_tensor(kind=0, seed=4)
-            s.setup()
+        lo, hi = s.tensor_planes()
+        z0, z1 = D.slabs(gshape, nranks)[r]
+        assert (lo, hi) == (max(z0 - 8, 0), min(z1 + 8, gshape[0]))  # O(slab) tensor
+        s.synth_tensor(kind=0, seed=4)
+        s.setup()
         assert s.num_levels == nlev
         return _drive(s, M), s.smooth_kernel_name(0)
 

@@ -38,3 +38,31 @@ def test_bootstrap_node_file_rendezvous(monkeypatch):
     assert len(set(got.values())) == 1 and len(got[0]) == 128
     from multigridanisotropicdiffusion_amd import distributed as D
     assert not os.path.exists(D._rdzv_path("cputest").replace(str(os.getppid()), str(os.getpid())))
+
+
+def test_rendezvous_key_carries_the_elastic_restart(monkeypatch):
+    """A torchrun restart keeps the agent pid and MASTER_PORT; the run id and restart count
+    make the restarted ranks meet in a fresh file (a dead rank 0's id is never read)."""
+    from multigridanisotropicdiffusion_amd import distributed as D
+    monkeypatch.setenv("MASTER_PORT", "29555")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job7")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    first = D._rdzv_path("sweep")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    second = D._rdzv_path("sweep")
+    assert first != second and "job7" in first
+    assert D._rdzv_path("vcycle") != second
+
+
+def test_bootstrap_node_fails_fast_without_launcher_env(monkeypatch):
+    from multigridanisotropicdiffusion_amd import distributed as D
+    monkeypatch.delenv("MASTER_PORT", raising=False)
+
+    class Never:
+        def comm_init(self, uid):
+            raise AssertionError("must not get here")
+    with pytest.raises(RuntimeError, match="MASTER_PORT"):
+        D.bootstrap_node(Never(), 1, 2, tag="x", timeout=0.1)
+    with pytest.raises(ValueError):
+        monkeypatch.setenv("MASTER_PORT", "1")
+        D.bootstrap_node(Never(), 3, 2, tag="x", timeout=0.1)
