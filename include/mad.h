@@ -78,6 +78,8 @@ typedef enum mad_precision {
   MAD_FP32 = 0, MAD_FP64 = 1, MAD_FP32_REFINE = 2, MAD_PRECISION_AUTO = 3
 } mad_precision;
 #define MAD_FP32_TOLERANCE_FLOOR 1e-6
+/* default mad_desc.min_slab_planes (measured: profiles/r03_agglomeration.md) */
+#define MAD_MIN_SLAB_PLANES 4
 
 typedef enum mad_tensor_kind {
   MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */
@@ -122,7 +124,11 @@ typedef struct mad_desc {
                                     the last z-chunk marched downward (the rank-slab single-
                                     launch form, selectable on one GPU for parity) */
   uint32_t options;              /* MAD_OPT_* bits, default 0 */
-  int32_t reserved[7];
+  int32_t min_slab_planes;       /* z-slab decomposition: a coarse level stays distributed while
+                                    every rank keeps >= this many planes of it (and >= 32x32x8
+                                    voxels); the first level below is replicated on every rank
+                                    (agglomeration).  0 = default (MAD_MIN_SLAB_PLANES) */
+  int32_t reserved[6];
 } mad_desc;
 
 /* mad_desc.options: MAD_OPT_EAGER_RANK_VCYCLE keeps a multi-rank V-cycle eager instead of

@@ -77,7 +77,8 @@ class MadDesc(ctypes.Structure):
         ("rank", ctypes.c_int32),
         ("gs_kernel", ctypes.c_int32),
         ("options", ctypes.c_uint32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("min_slab_planes", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 

@@ -2191,10 +2191,11 @@ std::vector<LevelGeom> plan_geometry(const mad_desc& d) {
     REQUIRE(geom[0].n[2] % P == 0 && geom[0].n[2] / P >= 4, MAD_ERR_INVALID,
             "z size must split into >= 4 planes per rank");
     REQUIRE(nlev >= 2, MAD_ERR_UNSUPPORTED, "multi-GPU needs at least two levels");
+    const int64_t minp = std::max(4, d.min_slab_planes > 0 ? d.min_slab_planes : MAD_MIN_SLAB_PLANES);
     int ld = 0;
     for (int l = 0; l < nlev - 1; ++l) {
       const LevelGeom& G = geom[l];
-      bool ok = (G.n[2] % P == 0) && (G.n[2] / P >= 4);
+      bool ok = (G.n[2] % P == 0) && (G.n[2] / P >= (l == 0 ? 4 : minp));
       for (int q = 1; q <= l; ++q) ok = ok && (geom[q].cent[2] == 1);
       if (!ok) break;
       ld = l;
@@ -2288,6 +2289,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
     REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
     REQUIRE((d->options & ~MAD_OPT_EAGER_RANK_VCYCLE) == 0, MAD_ERR_INVALID, "unknown option bits");
+    REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");
     c->d = *d;

@@ -123,6 +123,19 @@ def test_plan_slabs_cover_and_align(nranks):
     assert plans[0][nl - 1]["dist"] == 0
 
 
+@pytest.mark.parametrize("nranks,msp,depths", [
+    (8, 0, [64, 32, 16, 8, 4]), (8, 16, [64, 32, 16]), (8, 64, [64]),
+    (4, 8, [128, 64, 32, 16, 8]), (2, 32, [256, 128, 64, 32]),
+])
+def test_plan_min_slab_planes(nranks, msp, depths):
+    """mad_desc.min_slab_planes: coarse levels stay distributed while every rank keeps that many
+    planes (level 0 always: >= 4); the rest is replicated (agglomeration)."""
+    from multigridanisotropicdiffusion_amd import distributed as D
+    p = D.plan((512, 512, 512), nranks, nranks - 1, msp)
+    assert [q["z1"] - q["z0"] for q in p if q["distributed"]] == depths
+    assert all(not q["distributed"] for q in p[len(depths):])
+
+
 def test_plan_rejects_bad_slab_requests():
     with pytest.raises(C.MadError):
         _plan((510, 512, 512), nranks=4)  # 510 planes do not split into 4
