@@ -100,6 +100,23 @@ def cpu_baseline(seconds):
     out["parallel"] = {"value": nvox * m / el2 / 1e6, "unit": "Mvoxel-smooths/s", "cores": nt,
                        "kind": "port", "sample": f"128^3 VED-form full tensor, {m} 4-colour GS "
                        f"sweeps on {nt} OpenMP threads, fp64, oracle/, {el2:.1f} s"}
+    # the V-cycle line (BASELINE.md's C4 plan: fixed sweeps and V-cycles): whole V-cycles of
+    # the restated reference (MAD.hxx:341-493, nu = 2, lexicographic GS, 1 thread) on the
+    # 128^3 sample; the 512^3 figure scales it by the voxel count (the work is linear in N)
+    x = b.copy()
+    k = 0
+    t0 = time.perf_counter()
+    while True:
+        x = o.vcycle(x, b, smoother=oracle.GS_LEX, iterations_per_grid=2)
+        k += 1
+        el3 = time.perf_counter() - t0
+        if el3 >= seconds / 2:
+            break
+    out["vcycle"] = {"value": k / el3, "unit": "V-cycles/s (128^3 sample)", "cores": 1, "kind": "port",
+                     "value_512_equiv": k / el3 / 64.0,
+                     "sample": f"128^3 VED-form full tensor, {k} V-cycles (nu = 2, lexicographic GS, "
+                               f"{o.num_levels} levels), fp64, oracle/, {el3:.1f} s; value_512_equiv = "
+                               f"value / 64 (voxel count)"}
     return out
 
 
