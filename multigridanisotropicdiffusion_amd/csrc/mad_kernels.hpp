@@ -288,25 +288,37 @@ __global__ void __launch_bounds__(256) gs_brick_k(const T* __restrict__ uin, T* 
   const int nx = g.nx, ny = g.ny, nz = g.nz;
   const int zlo = g.zlo_ghost ? -GHOST : 0, zhi = g.zhi_ghost ? nz + GHOST : nz;
   // stage the region (points outside the grid / the valid planes are never read: every
-  // neighbour read is mirrored into the grid)
-  for (int q = tid; q < RZ * SXY; q += NT) {
+  // neighbour read is mirrored into the grid); loads batched ahead of the LDS stores
+  constexpr int RL = (RZ * SXY + NT - 1) / NT;
+#pragma unroll 6
+  for (int e = 0; e < RL; ++e) {
+    const int q = tid + e * NT;
     const int lk = q / SXY, r2 = q - lk * SXY, lj = r2 / RX, li = r2 - lj * RX;
     const int i = I0 - H + li, j = J0 - H + lj, k = K0 - H + lk;
-    if (i >= 0 && i < nx && j >= 0 && j < ny && k >= zlo && k < zhi)
+    if (q < RZ * SXY && i >= 0 && i < nx && j >= 0 && j < ny && k >= zlo && k < zhi)
       us[q] = uin[i + g.sy * j + g.sz * (int64_t)k];
   }
   __syncthreads();
+  constexpr int NCF = CoefLayout<3, KIND>::N;
+  // colour c's points of its box: per plane a half lattice in x (4 colours: and in y);
+  // a thread's points of one colour (at most PPT) load their records and b first, then update
+  constexpr int NIH = (BX + 2 * (NC - 1)) / 2 + 1;
+  constexpr int NJ = (NC == 4) ? (BY + 2 * (NC - 1)) / 2 + 1 : BY + 2 * (NC - 1);
+  constexpr int NKM = BZ + 2 * (NC - 1);
+  constexpr int PPT = (NKM * NJ * NIH + NT - 1) / NT;
   for (int c = 0; c < NC; ++c) {
     const int gc = NC - 1 - c;
     const int ib0 = max(I0 - gc, 0), ib1 = min(I0 + BX + gc, nx);
     const int jb0 = max(J0 - gc, 0), jb1 = min(J0 + BY + gc, ny);
     const int kb0 = max(K0 - gc, g.zlo_ghost ? -gc : 0);
     const int kb1 = min(K0 + BZ + gc, g.zhi_ghost ? nz + gc : nz);
-    // colour c's points of the box: per plane a half lattice in x (4 colours: and in y)
-    constexpr int NIH = (BX + 2 * (NC - 1)) / 2 + 1;
-    constexpr int NJ = (NC == 4) ? (BY + 2 * (NC - 1)) / 2 + 1 : BY + 2 * (NC - 1);
-    const int nk = kb1 - kb0;
-    for (int q = tid; q < nk * NJ * NIH; q += NT) {
+    const int nq = max(kb1 - kb0, 0) * NJ * NIH;
+    int pi_[PPT], pj_[PPT], pk_[PPT];
+    T raw[PPT][NCF];
+    T bv[PPT];
+#pragma unroll
+    for (int t = 0; t < PPT; ++t) {
+      const int q = tid + t * NT;
       const int kq = q / (NJ * NIH), r2 = q - kq * (NJ * NIH), jq = r2 / NIH, iq = r2 - jq * NIH;
       const int k = kb0 + kq;
       const int kg = k + g.zoff;
@@ -320,7 +332,21 @@ __global__ void __launch_bounds__(256) gs_brick_k(const T* __restrict__ uin, T* 
         const int pi = (c + j + kg) & 1;
         i = ib0 + ((pi - ib0) & 1) + 2 * iq;
       }
-      if (i >= ib1 || j >= jb1) continue;
+      const bool ok = q < nq && i < ib1 && j < jb1;
+      pi_[t] = ok ? i : -1;
+      pj_[t] = j;
+      pk_[t] = k;
+      if (ok) {
+        const T* rec = cf + cidx(g, i, j, k) * g.rs;
+#pragma unroll
+        for (int a = 0; a < NCF; ++a) raw[t][a] = rec[a];
+        bv[t] = b[i + g.sy * j + g.sz * (int64_t)k];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < PPT; ++t) {
+      const int i = pi_[t], j = pj_[t], k = pk_[t];
+      if (i < 0) continue;
       const int l0 = ((k - K0 + H) * RY + (j - J0 + H)) * RX + (i - I0 + H);
       const int dxm = (i == 0) ? 1 : -1;
       const int dxp = (i == nx - 1) ? -1 : 1;
@@ -350,10 +376,10 @@ __global__ void __launch_bounds__(256) gs_brick_k(const T* __restrict__ uin, T* 
         nb[17] = us[l0 + dym + dzm];
       }
       Coefs<T> cq;
-      load_coefs<T, 3, KIND>(cf, cidx(g, i, j, k), g.rs, rat, cq);
+      coefs_from_raw<T, 3, KIND>(raw[t], rat, cq);
       T D, S;
       stencil_combine<T, 3, KIND>(cq, nb, D, S);
-      us[l0] = gs_update(b[i + g.sy * j + g.sz * (int64_t)k], S, D);
+      us[l0] = gs_update(bv[t], S, D);
     }
     __syncthreads();
   }
