@@ -119,11 +119,11 @@ typedef struct mad_desc {
   int32_t nranks;                /* z-slab decomposition: number of ranks (1 = single GPU) */
   int32_t rank;                  /* this rank */
   int32_t gs_kernel;             /* 3D multicolour GS: 0 auto (fused single-launch sweep
-                                    gs_fused3_k on large levels, the whole-sweep brick kernel
-                                    gs_brick_k below), 1 one launch per colour, 3 gs_fused3_k,
-                                    4 gs_fused3_k with the last z-chunk marched downward (the
-                                    rank-slab single-launch form, selectable on one GPU for
-                                    parity), 5 gs_brick_k on every level; all bit-identical */
+                                    gs_fused3_k on large levels, one launch per colour below),
+                                    1 one launch per colour, 3 gs_fused3_k, 4 gs_fused3_k with
+                                    the last z-chunk marched downward (the rank-slab single-
+                                    launch form, selectable on one GPU for parity); all
+                                    bit-identical */
   uint32_t options;              /* MAD_OPT_* bits, default 0 */
   int32_t min_slab_planes;       /* z-slab decomposition: a coarse level stays distributed while
                                     every rank keeps >= this many planes of it (and >= 32x32x8

@@ -258,139 +258,6 @@ __global__ void __launch_bounds__(256) gs_color_k(T* __restrict__ u, const T* __
   u[p] = gs_update(b[p], S, D);
 }
 
-// ---------------------------------------------------------------------------
-// One whole multicolour GS sweep of a small 3D level in ONE launch (the coarse levels, where
-// the per-colour launches run at the per-launch floor): each workgroup owns a BX x BY x BZ
-// brick, stages the brick + NC points per side of u in LDS, runs the NC colour passes there --
-// colour c on the brick grown by NC - 1 - c (overlapped bricks: the points a neighbour's
-// later colours need are recomputed here from the same old values, so no workgroup waits for
-// another) -- and stores the brick, out of place (uin -> uout).  Neighbour reads are
-// gather_nb's mirror rule on LDS strides, records / b come from memory, the arithmetic is
-// stencil_combine + gs_update: bit-identical to NC in-place gs_color_k passes.  On a rank slab
-// the colours reach the NC - 1 - c nearest ghost planes as gs_color_k's communication-avoiding
-// passes do (one exchange of NC ghost planes per sweep).  Needs H = NC ghost planes of u and b
-// where zlo_ghost / zhi_ghost are set.
-template <typename T, int KIND, int BX, int BY, int BZ>
-__global__ void __launch_bounds__(256) gs_brick_k(const T* __restrict__ uin, T* __restrict__ uout,
-                                                  const T* __restrict__ b, const T* __restrict__ cf,
-                                                  Geo g, Rat<T> rat, int nbx, int nby) {
-  constexpr int NC = (KIND == KFULL) ? 4 : 2;
-  constexpr int H = NC;
-  constexpr int RX = BX + 2 * H, RY = BY + 2 * H, RZ = BZ + 2 * H;
-  constexpr int SXY = RX * RY;
-  constexpr int NT = 256;
-  __shared__ T us[RZ * SXY];
-  const int tid = threadIdx.x;
-  const int bz = blockIdx.x / (nbx * nby);
-  const int rem = blockIdx.x - bz * (nbx * nby);
-  const int byi = rem / nbx, bxi = rem - (rem / nbx) * nbx;
-  const int I0 = bxi * BX, J0 = byi * BY, K0 = bz * BZ;
-  const int nx = g.nx, ny = g.ny, nz = g.nz;
-  const int zlo = g.zlo_ghost ? -GHOST : 0, zhi = g.zhi_ghost ? nz + GHOST : nz;
-  // stage the region (points outside the grid / the valid planes are never read: every
-  // neighbour read is mirrored into the grid); loads batched ahead of the LDS stores
-  constexpr int RL = (RZ * SXY + NT - 1) / NT;
-#pragma unroll 6
-  for (int e = 0; e < RL; ++e) {
-    const int q = tid + e * NT;
-    const int lk = q / SXY, r2 = q - lk * SXY, lj = r2 / RX, li = r2 - lj * RX;
-    const int i = I0 - H + li, j = J0 - H + lj, k = K0 - H + lk;
-    if (q < RZ * SXY && i >= 0 && i < nx && j >= 0 && j < ny && k >= zlo && k < zhi)
-      us[q] = uin[i + g.sy * j + g.sz * (int64_t)k];
-  }
-  __syncthreads();
-  constexpr int NCF = CoefLayout<3, KIND>::N;
-  // colour c's points of its box: per plane a half lattice in x (4 colours: and in y);
-  // a thread's points of one colour (at most PPT) load their records and b first, then update
-  constexpr int NIH = (BX + 2 * (NC - 1)) / 2 + 1;
-  constexpr int NJ = (NC == 4) ? (BY + 2 * (NC - 1)) / 2 + 1 : BY + 2 * (NC - 1);
-  constexpr int NKM = BZ + 2 * (NC - 1);
-  constexpr int PPT = (NKM * NJ * NIH + NT - 1) / NT;
-  for (int c = 0; c < NC; ++c) {
-    const int gc = NC - 1 - c;
-    const int ib0 = max(I0 - gc, 0), ib1 = min(I0 + BX + gc, nx);
-    const int jb0 = max(J0 - gc, 0), jb1 = min(J0 + BY + gc, ny);
-    const int kb0 = max(K0 - gc, g.zlo_ghost ? -gc : 0);
-    const int kb1 = min(K0 + BZ + gc, g.zhi_ghost ? nz + gc : nz);
-    const int nq = max(kb1 - kb0, 0) * NJ * NIH;
-    int pi_[PPT], pj_[PPT], pk_[PPT];
-    T raw[PPT][NCF];
-    T bv[PPT];
-#pragma unroll
-    for (int t = 0; t < PPT; ++t) {
-      const int q = tid + t * NT;
-      const int kq = q / (NJ * NIH), r2 = q - kq * (NJ * NIH), jq = r2 / NIH, iq = r2 - jq * NIH;
-      const int k = kb0 + kq;
-      const int kg = k + g.zoff;
-      int i, j;
-      if (NC == 4) {
-        const int pi = (c ^ kg) & 1, pj = ((c >> 1) ^ kg) & 1;
-        i = ib0 + ((pi - ib0) & 1) + 2 * iq;
-        j = jb0 + ((pj - jb0) & 1) + 2 * jq;
-      } else {
-        j = jb0 + jq;
-        const int pi = (c + j + kg) & 1;
-        i = ib0 + ((pi - ib0) & 1) + 2 * iq;
-      }
-      const bool ok = q < nq && i < ib1 && j < jb1;
-      pi_[t] = ok ? i : -1;
-      pj_[t] = j;
-      pk_[t] = k;
-      if (ok) {
-        const T* rec = cf + cidx(g, i, j, k) * g.rs;
-#pragma unroll
-        for (int a = 0; a < NCF; ++a) raw[t][a] = rec[a];
-        bv[t] = b[i + g.sy * j + g.sz * (int64_t)k];
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < PPT; ++t) {
-      const int i = pi_[t], j = pj_[t], k = pk_[t];
-      if (i < 0) continue;
-      const int l0 = ((k - K0 + H) * RY + (j - J0 + H)) * RX + (i - I0 + H);
-      const int dxm = (i == 0) ? 1 : -1;
-      const int dxp = (i == nx - 1) ? -1 : 1;
-      const int dym = (j == 0) ? RX : -RX;
-      const int dyp = (j == ny - 1) ? -RX : RX;
-      const int dzm = (k == 0 && !g.zlo_ghost) ? SXY : -SXY;
-      const int dzp = (k == nz - 1 && !g.zhi_ghost) ? -SXY : SXY;
-      T nb[18];
-      nb[0] = us[l0 + dxp];
-      nb[1] = us[l0 + dxm];
-      nb[2] = us[l0 + dyp];
-      nb[3] = us[l0 + dym];
-      nb[4] = us[l0 + dzp];
-      nb[5] = us[l0 + dzm];
-      if (KIND == KFULL) {
-        nb[6] = us[l0 + dxp + dyp];
-        nb[7] = us[l0 + dxp + dym];
-        nb[8] = us[l0 + dxm + dyp];
-        nb[9] = us[l0 + dxm + dym];
-        nb[10] = us[l0 + dxp + dzp];
-        nb[11] = us[l0 + dxp + dzm];
-        nb[12] = us[l0 + dxm + dzp];
-        nb[13] = us[l0 + dxm + dzm];
-        nb[14] = us[l0 + dyp + dzp];
-        nb[15] = us[l0 + dyp + dzm];
-        nb[16] = us[l0 + dym + dzp];
-        nb[17] = us[l0 + dym + dzm];
-      }
-      Coefs<T> cq;
-      coefs_from_raw<T, 3, KIND>(raw[t], rat, cq);
-      T D, S;
-      stencil_combine<T, 3, KIND>(cq, nb, D, S);
-      us[l0] = gs_update(bv[t], S, D);
-    }
-    __syncthreads();
-  }
-  for (int q = tid; q < BX * BY * BZ; q += NT) {
-    const int lk = q / (BX * BY), r2 = q - lk * (BX * BY), lj = r2 / BX, li = r2 - lj * BX;
-    const int i = I0 + li, j = J0 + lj, k = K0 + lk;
-    if (i < nx && j < ny && k < nz)
-      uout[i + g.sy * j + g.sz * (int64_t)k] = us[((lk + H) * RY + (lj + H)) * RX + (li + H)];
-  }
-}
-
 // exact lexicographic GS (reference order, itkMultigridGaussSeidelSmoother.hxx:67-106)
 // as hyperplane wavefronts t = i + 2j + 3k (3D) / i + 2j (2D): every lex-earlier
 // neighbour lies on an earlier hyperplane, every later one on a later hyperplane.

@@ -503,9 +503,9 @@ class Solver final : public SolverBase {
   static int64_t margin_elems(const Geo& g) { return 48 * g.sy + 512; }
 
   bool use_fused(int l) const {
-    const int v = c_->d.gs_kernel;  // 0 auto, 1 per-colour passes, 3 / 4 fused, 5 brick
+    const int v = c_->d.gs_kernel;  // 0 auto, 1 per-colour passes, 3 / 4 fused
     if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL) return false;
-    if (v == 1 || v == 5) return false;
+    if (v == 1) return false;
     if (v >= 2) return true;
     // auto: the fused sweep marches each tile column through z sequentially, so it
     // needs a large slab to fill the chip; below ~4M voxels one launch per colour is
@@ -640,8 +640,6 @@ class Solver final : public SolverBase {
         std::snprintf(buf, sizeof buf, "wj_k<%s, %d, %d>", tn, dim, kind);
     } else if (c_->d.smoother == MAD_GAUSS_SEIDEL_LEX) {
       std::snprintf(buf, sizeof buf, "gs_lex_plane_k<%s, %d, %d>", tn, dim, kind);
-    } else if (use_brick(l)) {
-      std::snprintf(buf, sizeof buf, "gs_brick_k<%s, %d, %d, %d, %d>", tn, kind, BRICK_X, BRICK_Y, BRICK_Z);
     } else if (!use_fused(l)) {
       std::snprintf(buf, sizeof buf, "gs_color_k<%s, %d, %d>", tn, dim, kind);
     } else {
@@ -803,42 +801,6 @@ class Solver final : public SolverBase {
   }
 
   // per-colour GS on a 3D rank slab with one halo exchange per sweep
-  // the whole-sweep brick kernel (gs_brick_k) on the 3D GS levels the fused sweep does not take
-  // (gs_kernel 0 auto and 5; gs_kernel 1 keeps one launch per colour)
-  bool use_brick(int l) const {
-    const int v = c_->d.gs_kernel;
-    if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL || use_fused(l)) return false;
-    return v == 0 || v == 5;
-  }
-  static constexpr int BRICK_X = 16, BRICK_Y = sizeof(T) == 4 ? 16 : 8, BRICK_Z = 8;
-  void brick_sweep(int l) {
-    LevelData<T>& L = lv_[l];
-    if (colour_ca(l)) {
-      halo(l, L.x, c_->ncolors);
-      if (!L.b_halo_ok) {
-        halo(l, L.b, GHOST);
-        L.b_halo_ok = true;
-      }
-    }
-    wait_all_pending();
-    const int nbx = (L.g.nx + BRICK_X - 1) / BRICK_X, nby = (L.g.ny + BRICK_Y - 1) / BRICK_Y;
-    const int nbz = (L.g.nz + BRICK_Z - 1) / BRICK_Z;
-    const dim3 gr((unsigned)(nbx * nby * nbz));
-    if (c_->kind == KFULL)
-      hipLaunchKernelGGL((gs_brick_k<T, KFULL, BRICK_X, BRICK_Y, BRICK_Z>), gr, dim3(256), 0, c_->stream, L.x,
-                         L.t, L.b, L.cf, L.g, L.rat, nbx, nby);
-    else if (c_->kind == KDIAG)
-      hipLaunchKernelGGL((gs_brick_k<T, KDIAG, BRICK_X, BRICK_Y, BRICK_Z>), gr, dim3(256), 0, c_->stream, L.x,
-                         L.t, L.b, L.cf, L.g, L.rat, nbx, nby);
-    else
-      hipLaunchKernelGGL((gs_brick_k<T, KISO, BRICK_X, BRICK_Y, BRICK_Z>), gr, dim3(256), 0, c_->stream, L.x,
-                         L.t, L.b, L.cf, L.g, L.rat, nbx, nby);
-    HIP_CHECK(hipGetLastError());
-    std::swap(L.x, L.t);
-    std::swap(L.alloc[0], L.alloc[3]);
-    x_changed(l);
-  }
-
   bool colour_ca(int l) const {
     return c_->dim == 3 && c_->comm.active() && c_->geom[l].distributed &&
            c_->ncolors <= GHOST;
@@ -869,8 +831,6 @@ class Solver final : public SolverBase {
         HIP_CHECK(hipGetLastError());
       } else if (use_fused(l)) {
         fused_sweep(l);
-      } else if (use_brick(l)) {
-        brick_sweep(l);
       } else {
         const int nc = c_->ncolors;
         const int rows = (nc == 4) ? (L.g.ny + 1) / 2 : L.g.ny;
@@ -2326,9 +2286,8 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "bad precision");
     REQUIRE(d->nranks >= 1 && d->rank >= 0 && d->rank < d->nranks, MAD_ERR_INVALID,
             "bad rank / nranks");
-    REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4 ||
-                d->gs_kernel == 5,
-            MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3, 4 or 5");
+    REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
+            MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
     REQUIRE((d->options & ~MAD_OPT_EAGER_RANK_VCYCLE) == 0, MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,

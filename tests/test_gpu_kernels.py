@@ -183,15 +183,14 @@ def test_fused_gs_sweep_is_bitwise_per_colour_passes(shape, tensor, prec, cycle)
     mirror ghosts in LDS) equals NC in-place colour passes bit for bit, including partial
     tiles, partial z-chunks, odd sizes and 3-point axes (both mirror images of one point); so
     does it with its last z-chunk run on the z-reflected view (gs_kernel 4, the rank-slab
-    single-launch form), and so does the whole-sweep brick kernel of the small levels
-    (gs_brick_k, gs_kernel 5 forces it on every level: overlapped bricks, all colours in LDS)."""
+    single-launch form)."""
     import multigridanisotropicdiffusion_amd as M
     import synth
     T = {"full": lambda: synth.random_spd(shape, seed=1),
          "diag": lambda: synth.random_spd(shape, seed=1, offdiag=False),
          "iso": lambda: synth.isotropic(shape)}[tensor]()
     outs = []
-    for variant in (1, 3, 4, 5):  # 4: the last z-chunk marched downward; 5: bricks
+    for variant in (1, 3, 4):  # 4: the last z-chunk marched downward
         s = M.Solver(shape, (1.0, 0.8, 1.3), time_step=0.7, precision=prec, gs_kernel=variant,
                      cycle=cycle)
         s.set_tensor(T)
