@@ -1042,8 +1042,13 @@ class Solver final : public SolverBase {
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
       else go(std::integral_constant<int, KISO>{});
     };
-    run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
-        std::integral_constant<int, 512>{});
+#ifndef MAD_RR_CX  // A/B builds of the descent tile (tools/ab_lib.sh); removed once chosen
+#define MAD_RR_CX 32
+#define MAD_RR_CY 8
+#define MAD_RR_NT 512
+#endif
+    run(std::integral_constant<int, MAD_RR_CX>{}, std::integral_constant<int, MAD_RR_CY>{},
+        std::integral_constant<int, MAD_RR_NT>{});
     HIP_CHECK(hipGetLastError());
     return true;
   }
