@@ -184,3 +184,83 @@ def test_gloo_world2_slab_protocols():
         _, _, (ra, rb), _, z0, z1, _ = out[r]
         np.testing.assert_array_equal(ra, ref[z0:z1])
         np.testing.assert_array_equal(rb, ref[z0:z1])
+
+
+# ---------------------------------------------------------------- deep ghost exchange (setup)
+# Comm::shift_planes (csrc/mad_comm.hpp), the partitioned setup's tensor ghost exchange: ghost
+# regions deeper than a slab are filled hop by hop -- hop h (D = (h - 1) nz, d = min(nz, TG - D))
+# sends planes [D, D + d) down (received at [nz + D, nz + D + d) by rank - 1) and
+# [nz - D - d, nz - D) up (received at [-D - d, -D) by rank + 1).  Restated here with the same
+# offsets over gloo send/recv; every rank must end with the global planes [z0 - TG, z1 + TG)
+# that exist, also where they come from two or three ranks away.
+
+def _shift_worker(rank, world, port, nzl, tg, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        nzg = nzl * world
+        glob = np.arange(nzg * 6, dtype=np.float64).reshape(nzg, 2, 3)  # plane k holds 6k..6k+5
+        z0 = rank * nzl
+        a = np.full((nzl + 2 * tg, 2, 3), -1.0)  # local plane p at a[tg + p]
+        a[tg:tg + nzl] = glob[z0:z0 + nzl]
+        has_lo, has_hi = rank > 0, rank < world - 1
+        D = 0
+        while D < tg:
+            d = min(nzl, tg - D)
+            reqs = []
+            if has_lo:  # down: [D, D + d) to rank - 1
+                reqs.append(dist.isend(torch.from_numpy(a[tg + D:tg + D + d].copy()), rank - 1))
+            if has_hi:  # up: [nz - D - d, nz - D) to rank + 1
+                reqs.append(dist.isend(torch.from_numpy(a[tg + nzl - D - d:tg + nzl - D].copy()), rank + 1))
+            if has_lo:  # from below into [-D - d, -D)
+                buf = torch.zeros((d, 2, 3), dtype=torch.float64)
+                dist.recv(buf, rank - 1)
+                a[tg - D - d:tg - D] = buf.numpy()
+            if has_hi:  # from above into [nz + D, nz + D + d)
+                buf = torch.zeros((d, 2, 3), dtype=torch.float64)
+                dist.recv(buf, rank + 1)
+                a[tg + nzl + D:tg + nzl + D + d] = buf.numpy()
+            for r in reqs:
+                r.wait()
+            D += d
+        q.put((rank, a, z0, None))
+        dist.destroy_process_group()
+    except BaseException:  # noqa: BLE001
+        q.put((rank, None, 0, traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("nzl,tg", [(2, 8), (4, 8), (8, 8), (3, 5)])
+def test_gloo_world4_deep_ghost_exchange(nzl, tg):
+    import torch.multiprocessing as mp
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shift_worker, args=(r, world, port, nzl, tg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r = q.get(timeout=240)
+            assert r[3] is None, r[3]
+            out[r[0]] = r
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.terminate()
+    nzg = nzl * world
+    glob = np.arange(nzg * 6, dtype=np.float64).reshape(nzg, 2, 3)
+    for r in range(world):
+        _, a, z0, _ = out[r]
+        for p in range(-tg, nzl + tg):
+            k = z0 + p
+            if 0 <= k < nzg:
+                np.testing.assert_array_equal(a[tg + p], glob[k], err_msg=f"rank {r} plane {p}")
+            else:
+                assert (a[tg + p] == -1.0).all()  # outside the grid: never written
