@@ -111,6 +111,9 @@ int mad_ved_run_device(mad_ved_ctx *ctx, const void *in, int32_t in_dtype, void 
  * the in-process variant runs ranks as threads on one device (tests). */
 int mad_ved_comm_init(mad_ved_ctx *ctx, const void *uid128);
 int mad_ved_comm_init_local(mad_ved_ctx *ctx, uint64_t group);
+/* Measurement only (as mad_comm_init_solo): this rank alone on its device, every exchange a
+ * device copy of the same bytes -- one rank's share of a partitioned run, timed on one GPU. */
+int mad_ved_comm_init_solo(mad_ved_ctx *ctx);
 
 /* One tensor generation on a host image (parity / inspection): all scales of
  * ComputeHessian + UpdateVesselness, then GenerateDiffusionTensor.  tensor_soa: 6 arrays

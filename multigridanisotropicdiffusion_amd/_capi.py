@@ -48,6 +48,7 @@ EXPORTS = (
     # include/mad_ved.h
     "mad_ved_desc_init", "mad_ved_create", "mad_ved_destroy", "mad_ved_last_error",
     "mad_ved_run", "mad_ved_run_device", "mad_ved_comm_init", "mad_ved_comm_init_local",
+    "mad_ved_comm_init_solo",
     "mad_ved_tensor", "mad_ved_hessian",
 )
 
@@ -230,6 +231,7 @@ def load():
         "mad_ved_run_device": ([vp, vp, i32, vp, i32, ctypes.POINTER(VedStats)], i32),
         "mad_ved_comm_init": ([vp, vp], i32),
         "mad_ved_comm_init_local": ([vp, ctypes.c_uint64], i32),
+        "mad_ved_comm_init_solo": ([vp], i32),
         "mad_ved_tensor": ([vp, vp, i32, dp, dp], i32),
         "mad_ved_hessian": ([vp, vp, i32, dbl, dp], i32),
     }

@@ -274,6 +274,40 @@ class Comm {
     group_->barrier();
   }
 
+  // All-to-all of device buffers (the partitioned VED's transpose): send[r] (sbytes[r]) goes to
+  // rank r, recv[q] (rbytes[q]) comes from rank q; entries of this rank are not moved.  Byte
+  // counts are multiples of 4 (fp32 / fp64 volumes).
+  void exchange_blocks(const std::vector<const void*>& send, const std::vector<size_t>& sbytes,
+                       const std::vector<void*>& recv, const std::vector<size_t>& rbytes, hipStream_t s) {
+    if (mode_ == RCCL) {
+      NCCL_CHECK(ncclGroupStart());
+      for (int r = 0; r < nranks_; ++r) {
+        if (r == rank_) continue;
+        if (sbytes[r]) NCCL_CHECK(ncclSend(send[r], sbytes[r] / 4, ncclFloat, r, comm_, s));
+        if (rbytes[r]) NCCL_CHECK(ncclRecv(recv[r], rbytes[r] / 4, ncclFloat, r, comm_, s));
+      }
+      NCCL_CHECK(ncclGroupEnd());
+      return;
+    }
+    if (mode_ == SOLO) {  // the same bytes: this rank's own blocks stand in for the peers'
+      for (int r = 0; r < nranks_; ++r)
+        if (r != rank_ && rbytes[r])
+          HIPC_CHECK(hipMemcpyAsync(recv[r], send[r], std::min(sbytes[r], rbytes[r]), hipMemcpyDeviceToDevice, s));
+      return;
+    }
+    // LOCAL: publish the send table, pull every peer's block addressed to this rank
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->ptr[rank_] = (void*)send.data();
+    group_->barrier();
+    for (int q = 0; q < nranks_; ++q) {
+      if (q == rank_ || !rbytes[q]) continue;
+      const void* const* peer = (const void* const*)group_->ptr[q];
+      HIPC_CHECK(hipMemcpyAsync(recv[q], peer[rank_], rbytes[q], hipMemcpyDeviceToDevice, s));
+    }
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->barrier();
+  }
+
   void allreduce_sum_f64(double* p, size_t n, hipStream_t s) {
     if (mode_ == RCCL) {
       NCCL_CHECK(ncclAllReduce(p, p, n, ncclDouble, ncclSum, comm_, s));

@@ -23,10 +23,12 @@ struct mad_ved_ctx {
   double* dir = nullptr;   // vessel direction (eigenvector column 2 of the max scale), SoA x3
   void* stage = nullptr;   // host <-> device staging
   size_t stage_bytes = 0;
+  void* xbuf = nullptr;    // send + receive blocks of the partitioned Hessian's transpose
+  size_t xbuf_bytes = 0;
   ~mad_ved_ctx() {
     if (mad) (void)hipSetDevice(mad->device);
     if (mad && mad->stream) (void)hipStreamSynchronize(mad->stream);
-    for (void* p : {(void*)img, (void*)img2, fir, (void*)iir, taps, (void*)resp, (void*)dir, stage})
+    for (void* p : {(void*)img, (void*)img2, fir, (void*)iir, taps, (void*)resp, (void*)dir, stage, xbuf})
       if (p) (void)hipFree(p);
     if (mad) mad_destroy(mad);
   }
@@ -215,9 +217,17 @@ IirCoef ved_iir_coef(double sd, int order) {
 
 // one scale with the recursive (IIR) operator: z pass (image -> orders 0..2), y pass (-> the
 // six (y, z) order pairs), x pass (-> the six scaled Hessian components), then the Hessian
-// out (VED_HESSIAN) or UpdateVesselness (VED_UPDATE) per voxel
+// out (VED_HESSIAN) or UpdateVesselness (VED_UPDATE) per voxel.
+// Partitioned (dist: a z-slab rank of the VED run): every z line lies in one x column, every
+// y and x line in one z plane, so rank r runs the z pass on its x range [xa_r, xb_r) (all
+// planes), the three z-pass volumes are transposed -- rank r sends each rank q the block [q's
+// tensor planes] x [all y] x [xa_r, xb_r) (Comm::exchange_blocks) -- and the y pass, the x pass
+// and the vesselness update run on the rank's tensor planes only (its slab + the TENSOR_GHOST
+// planes the solver's tensor slab holds).  Each line sees the same values through the same
+// expressions, so the tensor equals the one-GPU tensor bit for bit, at 1 / P of the passes'
+// work plus the transpose.
 template <typename T>
-void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess) {
+void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess, bool dist = false) {
   hipStream_t st = v->mad->stream;
   const int nx = (int)v->n[0], ny = (int)v->n[1], nz = (int)v->n[2];
   REQUIRE(nx >= 4 && ny >= 4 && nz >= 4, MAD_ERR_UNSUPPORTED,
@@ -237,8 +247,18 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
   }
   const double* h = v->d.spacing;
   // MAD_VED_OPT_LINE_WALK (the parity reference): ved_iir_k's one thread per line for every
-  // axis, each output marched on its own
+  // axis, each output marched on its own (whole grid: not partitioned)
   const bool line_walk = (v->d.options & MAD_VED_OPT_LINE_WALK) != 0;
+  mad_ctx* c = v->mad;
+  dist = dist && !line_walk && c->comm.active() && c->d.nranks > 1;
+  const int P_ = dist ? c->d.nranks : 1, me = dist ? c->comm.rank() : 0;
+  auto xr = [&](int r) { return std::make_pair((int)((int64_t)nx * r / P_), (int)((int64_t)nx * (r + 1) / P_)); };
+  auto tplanes = [&](int r) {  // the tensor planes of rank r (compute_geometry's tensor slab)
+    if (!dist) return std::make_pair(0, nz);
+    const int per = nz / P_;
+    return std::make_pair(std::max(per * r - TENSOR_GHOST, 0), std::min(per * (r + 1) + TENSOR_GHOST, nz));
+  };
+  const int xa = xr(me).first, nxr = xr(me).second - xr(me).first;
   // SI: the z pass reads the fp64 image, the others the T volumes
   auto launch = [&](const IirPass& P, int axis, auto si) {
     using SI = decltype(si);
@@ -251,11 +271,20 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
       // chunk rows of one 128-B line (3.76 vs 4.15 ms per 512^3 fp32 pass with 64 B)
       if constexpr (std::is_same<SI, T>::value) {
         const dim3 gr((unsigned)((lines + 63) / 64), (unsigned)P.nout);
-        hipLaunchKernelGGL((ved_iir_x_k<SI, T, 128 / (int)sizeof(T)>), gr, dim3(64), 0, st, P, nx, lines);
+        const int64_t lb = (int64_t)tplanes(me).first * ny, le = (int64_t)tplanes(me).second * ny;
+        const dim3 grl((unsigned)((le - lb + 63) / 64), (unsigned)P.nout);
+        (void)gr;
+        hipLaunchKernelGGL((ved_iir_x_k<SI, T, 128 / (int)sizeof(T)>), grl, dim3(64), 0, st, P, nx, lb, le);
       }
     } else {
-      // strided lines: the outputs sharing an input in one march, one launch per input
-      const unsigned nb = (unsigned)((lines + 255) / 256);
+      // strided lines: the outputs sharing an input in one march, one launch per input; when
+      // partitioned, the z pass on the rank's x range (all y), the y pass on its tensor planes
+      // (all x)
+      const int lxa = (axis == 2) ? xa : 0, lnx = (axis == 2) ? nxr : nx;
+      const int lza = (axis == 1) ? tplanes(me).first : 0;
+      const int lnz = (axis == 1) ? tplanes(me).second - tplanes(me).first : nz;
+      const int64_t xl = (int64_t)lnx * (axis == 1 ? lnz : ny);
+      const unsigned nb = (unsigned)((xl + 255) / 256);
       bool done[6] = {false, false, false, false, false, false};
       for (int o = 0; o < P.nout; ++o) {
         if (done[o]) continue;
@@ -274,7 +303,12 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
             G.c[q] = P.c[outs[q]];
             G.scale[q] = P.scale[outs[q]];
           }
-          hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz);
+          if (dist)  // few lines per GPU: two load blocks in flight per line
+            hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K, 8, true>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz,
+                               lxa, lnx, lza, lnz);
+          else
+            hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz, lxa,
+                               lnx, lza, lnz);
         };
         if (k == 3) go(std::integral_constant<int, 3>{});
         else if (k == 2) go(std::integral_constant<int, 2>{});
@@ -294,6 +328,52 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     P.scale[o] = 1.0;
   }
   launch(P, 2, double{});
+  if (dist) {
+    // transpose the three z-pass volumes: the rank's x range (all planes) -> its tensor planes
+    // (all x); every y and x line then lies in the rank's planes
+    std::vector<const void*> sp(P_, nullptr);
+    std::vector<void*> rp(P_, nullptr);
+    std::vector<size_t> sb(P_, 0), rb(P_, 0);
+    const auto mp = tplanes(me);
+    size_t tot = 0;
+    for (int r = 0; r < P_; ++r) {
+      if (r == me) continue;
+      const auto tp = tplanes(r);
+      sb[r] = sizeof(T) * 3 * (size_t)(tp.second - tp.first) * ny * nxr;
+      rb[r] = sizeof(T) * 3 * (size_t)(mp.second - mp.first) * ny * (xr(r).second - xr(r).first);
+      tot += sb[r] + rb[r];
+    }
+    if (tot > v->xbuf_bytes) {
+      if (v->xbuf) HIP_CHECK(hipFree(v->xbuf));
+      v->xbuf = nullptr;
+      HIP_CHECK(hipMalloc(&v->xbuf, tot));
+      v->xbuf_bytes = tot;
+    }
+    Vol6<T> Z3{};
+    for (int q = 0; q < 3; ++q) Z3.v[q] = Z[q];
+    char* cur = (char*)v->xbuf;
+    for (int r = 0; r < P_; ++r) {
+      if (r == me) continue;
+      sp[r] = cur;
+      cur += sb[r];
+      rp[r] = cur;
+      cur += rb[r];
+      const auto tp = tplanes(r);
+      const int nzb = tp.second - tp.first;
+      hipLaunchKernelGGL((ved_block_k<T, false>), dim3(flat_blocks(3 * (int64_t)nzb * ny * nxr)), dim3(256), 0, st,
+                         Z3, (T*)sp[r], nx, ny, xa, nxr, tp.first, nzb, 3);
+    }
+    HIP_CHECK(hipGetLastError());
+    c->comm.exchange_blocks(sp, sb, rp, rb, st);
+    const int nzm = mp.second - mp.first;
+    for (int q = 0; q < P_; ++q) {
+      if (q == me) continue;
+      const int qa = xr(q).first, qn = xr(q).second - xr(q).first;
+      hipLaunchKernelGGL((ved_block_k<T, true>), dim3(flat_blocks(3 * (int64_t)nzm * ny * qn)), dim3(256), 0, st, Z3,
+                         (T*)rp[q], nx, ny, qa, qn, mp.first, nzm, 3);
+    }
+    HIP_CHECK(hipGetLastError());
+  }
   // y: (oy, oz) = (0,0) (1,0) (2,0) (0,1) (1,1) (0,2)
   const int pairs[6][2] = {{0, 0}, {1, 0}, {2, 0}, {0, 1}, {1, 1}, {0, 2}};
   P = IirPass{};
@@ -323,21 +403,22 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
   launch(P, 0, T{});
   const T* Hs = H[0];
   const VesselParams vp{v->d.alpha, v->d.beta, v->d.gamma};
-  const unsigned nb = flat_blocks(N);
+  const int64_t p0 = (int64_t)tplanes(me).first * nx * ny, p1 = (int64_t)tplanes(me).second * nx * ny;
+  const unsigned nb = flat_blocks(p1 - p0);
   if (mode == VED_HESSIAN)
-    hipLaunchKernelGGL((ved_hess_k<T, VED_HESSIAN, T>), dim3(nb), dim3(256), 0, st, Hs, N, hess, nullptr,
+    hipLaunchKernelGGL((ved_hess_k<T, VED_HESSIAN, T>), dim3(nb), dim3(256), 0, st, Hs, N, p0, p1, hess, nullptr,
                        nullptr, 0, vp);
   else
-    hipLaunchKernelGGL((ved_hess_k<T, VED_UPDATE, T>), dim3(nb), dim3(256), 0, st, Hs, N, nullptr, v->resp,
-                       v->dir, first ? 1 : 0, vp);
+    hipLaunchKernelGGL((ved_hess_k<T, VED_UPDATE, T>), dim3(nb), dim3(256), 0, st, Hs, N, p0, p1, nullptr,
+                       v->resp, v->dir, first ? 1 : 0, vp);
   HIP_CHECK(hipGetLastError());
 }
 
 // one scale: Hessian (MODE VED_HESSIAN, into `hess`) or vesselness update
 template <typename T>
-void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess) {
+void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess, bool dist = false) {
   if (v->d.hessian == MAD_VED_HESSIAN_RECURSIVE) {
-    ved_scale_iir<T>(v, sigma, mode, first, hess);
+    ved_scale_iir<T>(v, sigma, mode, first, hess, dist);
     return;
   }
   hipStream_t st = v->mad->stream;
@@ -402,7 +483,9 @@ void ved_tensor_impl(mad_ved_ctx* v) {
   const int64_t N = v->N;
   if (!v->resp) HIP_CHECK(hipMalloc(&v->resp, sizeof(double) * N));
   if (!v->dir) HIP_CHECK(hipMalloc(&v->dir, sizeof(double) * 3 * N));
-  for (int s = 0; s < v->d.nscales; ++s) ved_scale<T>(v, v->d.scales[s], VED_UPDATE, s == 0, nullptr);
+  // the run's tensor: partitioned across the ranks (recursive Hessian; the FIR operator and
+  // the line-walk reference stay whole-grid on every rank)
+  for (int s = 0; s < v->d.nscales; ++s) ved_scale<T>(v, v->d.scales[s], VED_UPDATE, s == 0, nullptr, true);
   // the tensor planes this rank's solver stores (its slab + ghost planes; all on one GPU)
   tensor_alloc(c);
   const int64_t sz = v->n[0] * v->n[1];
@@ -611,6 +694,11 @@ int mad_ved_comm_init(mad_ved_ctx* v, const void* uid128) {
 int mad_ved_comm_init_local(mad_ved_ctx* v, uint64_t group) {
   if (!v) return MAD_ERR_INVALID;
   return ved_guarded(v, [&] { mad_call(v->mad, mad_comm_init_local(v->mad, group)); });
+}
+
+int mad_ved_comm_init_solo(mad_ved_ctx* v) {
+  if (!v) return MAD_ERR_INVALID;
+  return ved_guarded(v, [&] { mad_call(v->mad, mad_comm_init_solo(v->mad)); });
 }
 
 int mad_ved_tensor(mad_ved_ctx* v, const void* image, int32_t dtype, double* tensor_soa,

@@ -558,22 +558,29 @@ struct IirGroup {
   double scale[K];
 };
 
-template <typename SI, typename SO, int K>
-__global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, int nx, int ny, int nz) {
+// Lines of the x columns [xa, xa + nxr) (z lines: all y; y lines: the planes [za, za + nzr))
+// only -- the whole grid: xa = 0, nxr = nx, za = 0, nzr = nz: a rank of the partitioned VED
+// runs the z pass on its x range and the y pass on its tensor planes (ved_scale_iir).  B:
+// points per load block (16 and more put the blocks in scratch memory); PIPE: the next block's
+// loads are issued before the current block is filtered (two blocks in flight per line -- the
+// partitioned passes have few lines per GPU, so each line's round trips are the time).
+template <typename SI, typename SO, int K, int B = 8, bool PIPE = false>
+__global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, int nx, int ny, int nz,
+                                                     int xa, int nxr, int za, int nzr) {
 #pragma clang fp contract(off)
-  constexpr int B = 8;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t base, st;
   int n;
   if (axis == 1) {  // along y, one per (x, z)
-    if (t >= (int64_t)nx * nz) return;
-    const int64_t i = t % nx, k = t / nx;
+    if (t >= (int64_t)nxr * nzr) return;
+    const int64_t i = xa + t % nxr, k = za + t / nxr;
     base = k * nx * ny + i;
     st = nx;
     n = ny;
   } else {  // along z, one per (x, y)
-    if (t >= (int64_t)nx * ny) return;
-    base = t;
+    if (t >= (int64_t)nxr * ny) return;
+    const int64_t i = xa + t % nxr, j = t / nxr;
+    base = j * nx + i;
     st = (int64_t)nx * ny;
     n = nz;
   }
@@ -605,10 +612,23 @@ __global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, in
       sm1[q] = s3; sm2[q] = s2; sm3[q] = s1; sm4[q] = s0;
     }
     double xm1 = x3, xm2 = x2, xm3 = x1;
+    SI xn[B];
+    if (PIPE) {
+#pragma unroll
+      for (int u = 0; u < B; ++u) xn[u] = (4 + u < n) ? x[(int64_t)(4 + u) * st] : SI(0);
+    }
     for (int i0 = 4; i0 < n; i0 += B) {
       SI xb[B];
+      if (PIPE) {
 #pragma unroll
-      for (int u = 0; u < B; ++u) xb[u] = (i0 + u < n) ? x[(int64_t)(i0 + u) * st] : SI(0);
+        for (int u = 0; u < B; ++u) {
+          xb[u] = xn[u];
+          xn[u] = (i0 + B + u < n) ? x[(int64_t)(i0 + B + u) * st] : SI(0);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < B; ++u) xb[u] = (i0 + u < n) ? x[(int64_t)(i0 + u) * st] : SI(0);
+      }
 #pragma unroll
       for (int u = 0; u < B; ++u) {
         const int i = i0 + u;
@@ -653,16 +673,42 @@ __global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, in
       b0[q] = a4; b1[q] = a3; b2[q] = a2; b3[q] = a1;
     }
     double w0 = x[(int64_t)(n - 4) * st], w1 = xc, w2 = xb, w3 = xa;
-    // blocks of B points downward from i = n-4 (point i-1 each step), loads first
+    // blocks of B points downward from i = n-4 (point i-1 each step), loads first (PIPE: the
+    // next block's loads ahead; they read causal outputs below the block being finished)
+    SI xpn[B];
+    SO ybn[K][B];
+    if (PIPE) {
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int i = n - 4 - u;
+        xpn[u] = (i > 0) ? x[(int64_t)(i - 1) * st] : SI(0);
+#pragma unroll
+        for (int q = 0; q < K; ++q) ybn[q][u] = (i > 0) ? y[q][(int64_t)(i - 1) * st] : SO(0);
+      }
+    }
     for (int i0 = n - 4; i0 > 0; i0 -= B) {
       SI xp[B];
       SO yb[K][B];
+      if (PIPE) {
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const int i = i0 - u;
-        xp[u] = (i > 0) ? x[(int64_t)(i - 1) * st] : SI(0);
+        for (int u = 0; u < B; ++u) {
+          const int i = i0 - B - u;
+          xp[u] = xpn[u];
+          xpn[u] = (i > 0) ? x[(int64_t)(i - 1) * st] : SI(0);
 #pragma unroll
-        for (int q = 0; q < K; ++q) yb[q][u] = (i > 0) ? y[q][(int64_t)(i - 1) * st] : SO(0);
+          for (int q = 0; q < K; ++q) {
+            yb[q][u] = ybn[q][u];
+            ybn[q][u] = (i > 0) ? y[q][(int64_t)(i - 1) * st] : SO(0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const int i = i0 - u;
+          xp[u] = (i > 0) ? x[(int64_t)(i - 1) * st] : SI(0);
+#pragma unroll
+          for (int q = 0; q < K; ++q) yb[q][u] = (i > 0) ? y[q][(int64_t)(i - 1) * st] : SO(0);
+        }
       }
 #pragma unroll
       for (int u = 0; u < B; ++u) {
@@ -690,8 +736,10 @@ __global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, in
 // recursion, same expressions in the same order as ved_iir_k (bit-identical): the causal
 // and anticausal passes are written as per-point state machines over a sliding window,
 // with the first four points of each direction taking ved_iir_k's edge formulas.
+// lines [lbase, nlines) (x rows, row index j + ny k): all of them on one GPU, a rank's tensor
+// planes in the partitioned VED
 template <typename SI, typename SO, int C = 128 / (int)sizeof(SO)>
-__global__ void __launch_bounds__(64) ved_iir_x_k(IirPass P, int nx, int64_t nlines) {
+__global__ void __launch_bounds__(64) ved_iir_x_k(IirPass P, int nx, int64_t lbase, int64_t nlines) {
 #pragma clang fp contract(off)
   static_assert(sizeof(SI) == sizeof(SO), "the x pass reads and writes the volumes' storage type");
   static_assert(64 % C == 0, "whole rows per wave instruction");
@@ -702,7 +750,7 @@ __global__ void __launch_bounds__(64) ved_iir_x_k(IirPass P, int nx, int64_t nli
   constexpr int RPI = 64 / C;  // rows per wave instruction
   const int o = blockIdx.y;
   const int lane = threadIdx.x;
-  const int64_t line0 = (int64_t)blockIdx.x * 64;
+  const int64_t line0 = lbase + (int64_t)blockIdx.x * 64;
   const SI* __restrict__ x = static_cast<const SI*>(P.in[P.src[o]]);
   SO* __restrict__ y = static_cast<SO*>(P.out[o]);
   const IirCoef c = P.c[o];
@@ -843,14 +891,37 @@ __global__ void __launch_bounds__(64) ved_iir_x_k(IirPass P, int nx, int64_t nli
 }
 
 // UpdateVesselness / Hessian output from the six recursive-Hessian volumes
+// (points [p0, p1) of the n-point volumes)
 template <typename T, int MODE, typename S = double>
-__global__ void __launch_bounds__(256) ved_hess_k(const S* __restrict__ H, int64_t n,
+__global__ void __launch_bounds__(256) ved_hess_k(const S* __restrict__ H, int64_t n, int64_t p0, int64_t p1,
                                                   double* __restrict__ hess, double* __restrict__ resp,
                                                   double* __restrict__ dir, int first, VesselParams vp) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+  for (int64_t p = p0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < p1;
        p += (int64_t)gridDim.x * blockDim.x)
     ved_point<T, MODE>(H[p], H[n + p], H[2 * n + p], H[3 * n + p], H[4 * n + p], H[5 * n + p], p, n,
                        hess, resp, dir, first, vp);
+}
+
+// Partitioned VED transpose: six volumes' block [z0, z0 + nzb) x [0, ny) x [x0, x0 + nxb) to or
+// from a contiguous buffer (volume-major, then z, y, x), UNPACK = buffer -> volumes.
+template <typename T>
+struct Vol6 {
+  T* v[6];
+};
+// nv volumes, one element per thread over the whole block (32-bit indices: a block holds < 2^31
+// elements), grid-stride
+template <typename T, bool UNPACK>
+__global__ void __launch_bounds__(256) ved_block_k(Vol6<T> V, T* __restrict__ buf, int nx, int ny, int x0,
+                                                   int nxb, int z0, int nzb, int nv) {
+  const uint32_t tot = (uint32_t)nv * nzb * ny * nxb;
+  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < tot; q += gridDim.x * 256u) {
+    const uint32_t row = q / (uint32_t)nxb, i = q - row * (uint32_t)nxb;
+    const uint32_t ck = row / (uint32_t)ny, j = row - ck * (uint32_t)ny;
+    const uint32_t c = ck / (uint32_t)nzb, kl = ck - c * (uint32_t)nzb;
+    T* vp = V.v[c] + ((int64_t)(z0 + (int)kl) * ny + j) * nx + x0 + i;
+    if (UNPACK) *vp = buf[q];
+    else buf[q] = *vp;
+  }
 }
 
 // GenerateDiffusionTensor (VED.hxx:302-378) into the solver's fp64 SoA tensor

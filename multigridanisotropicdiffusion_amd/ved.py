@@ -84,6 +84,10 @@ class VED:
         """In-process transport: ranks as threads of this process on one device."""
         self._check(self._L.mad_ved_comm_init_local(self._ctx, ctypes.c_uint64(group)))
 
+    def comm_init_solo(self):
+        """Measurement only (mad_ved_comm_init_solo): one rank alone on its device."""
+        self._check(self._L.mad_ved_comm_init_solo(self._ctx))
+
     def _check(self, rc):
         if rc != C.OK:
             raise C.MadError(rc, (self._L.mad_ved_last_error(self._ctx) or b"").decode())

@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--fp64", action="store_true")
+    ap.add_argument("--ranks", type=int, default=1,
+                    help="> 1: one interior rank (ranks // 2) of that decomposition alone on the device "
+                         "(mad_ved_comm_init_solo): its partitioned tensor generation and slab diffusion")
     ap.add_argument("--hessian", action="store_true",
                     help="also run one Hessian-only pass (profiling the FIR without the eigen stage)")
     a = ap.parse_args()
@@ -54,18 +57,25 @@ def main():
     img = phantom(S)
     t_ph = time.perf_counter() - t0
     prec = M.FP64 if a.fp64 else M.FP32
+    rk = dict(nranks=a.ranks, rank=a.ranks // 2) if a.ranks > 1 else {}
     v = M.VED((S, S, S), (1.0, 1.0, 1.0), omega=1.5, diffusion_iterations=a.steps,
-              precision=prec)
-    if a.hessian:
+              precision=prec, **rk)
+    if a.ranks > 1:
+        v.comm_init_solo()
+    if a.hessian and a.ranks == 1:
         v.hessian(img, 2.0)
     # tensor generation only (device time from the run's stats is below; here wall)
-    v.tensor(img)  # warm-up (allocations)
-    tw = []
-    for _ in range(a.reps):
-        t0 = time.perf_counter()
-        v.tensor(img)
-        tw.append(time.perf_counter() - t0)
+    tw = [float("nan")]
+    if a.ranks == 1:
+        v.tensor(img)  # warm-up (allocations)
+        tw = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            v.tensor(img)
+            tw.append(time.perf_counter() - t0)
     runs = []
+    if a.ranks > 1:
+        v.run(img, out_dtype=np.float32)  # warm-up (allocations, first eager cycles)
     for _ in range(a.reps):
         t0 = time.perf_counter()
         out, st = v.run(img, out_dtype=np.float32)
@@ -75,6 +85,7 @@ def main():
     N = float(S) ** 3
     print(json.dumps({
         "workload": f"VED {S}^3 tube phantom, 5 scales, 1 iteration, {a.steps} diffusion steps",
+        "ranks": a.ranks, "rank": a.ranks // 2 if a.ranks > 1 else 0,
         "precision": "fp64" if a.fp64 else "fp32",
         "tensor_wall_ms_incl_pcie": round(min(tw) * 1e3, 2),
         "tensor_device_ms": round(best["tensor_ms"], 3),
