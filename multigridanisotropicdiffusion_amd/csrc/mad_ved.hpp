@@ -303,12 +303,10 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
             G.c[q] = P.c[outs[q]];
             G.scale[q] = P.scale[outs[q]];
           }
-          if (dist)  // few lines per GPU: two load blocks in flight per line
-            hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K, 8, true>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz,
-                               lxa, lnx, lza, lnz);
-          else
-            hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz, lxa,
-                               lnx, lza, lnz);
+          // two load blocks in flight per line (512^3 tensor generation 65.0 -> 56.3 ms on one GPU,
+          // profiles/r03_ved_pipe_ab.log; the partitioned passes' few lines per GPU need it most)
+          hipLaunchKernelGGL((ved_iir_grp_k<SI, T, K, 8, true>), dim3(nb), dim3(256), 0, st, G, axis, nx, ny, nz,
+                             lxa, lnx, lza, lnz);
         };
         if (k == 3) go(std::integral_constant<int, 3>{});
         else if (k == 2) go(std::integral_constant<int, 2>{});

@@ -562,8 +562,8 @@ struct IirGroup {
 // only -- the whole grid: xa = 0, nxr = nx, za = 0, nzr = nz: a rank of the partitioned VED
 // runs the z pass on its x range and the y pass on its tensor planes (ved_scale_iir).  B:
 // points per load block (16 and more put the blocks in scratch memory); PIPE: the next block's
-// loads are issued before the current block is filtered (two blocks in flight per line -- the
-// partitioned passes have few lines per GPU, so each line's round trips are the time).
+// loads are issued before the current block is filtered (two blocks in flight per line: each
+// line's memory round trips are the time, most of all in the partitioned passes' few lines).
 template <typename SI, typename SO, int K, int B = 8, bool PIPE = false>
 __global__ void __launch_bounds__(256) ved_iir_grp_k(IirGroup<K> G, int axis, int nx, int ny, int nz,
                                                      int xa, int nxr, int za, int nzr) {
