@@ -135,6 +135,14 @@ typedef struct mad_desc {
 /* mad_desc.options: MAD_OPT_EAGER_RANK_VCYCLE keeps a multi-rank V-cycle eager instead of
    replaying its captured hipGraph (the reference of the graph-replay parity test) */
 #define MAD_OPT_EAGER_RANK_VCYCLE 1u
+/* Rank-slab fused sweeps come in two forms: split (boundary chunks, then the halo exchange on a
+   communication stream beside the interior launch) and serial (one launch, then the exchange on
+   the solver's stream).  By default mad_smooth uses the split and V-cycles / FMG the serial form
+   (a second stream inside the captured cycle graph slows every node's launch).
+   MAD_OPT_SERIAL_RANK_SWEEP makes every rank sweep serial; MAD_OPT_OVERLAP_RANK_CYCLE keeps the
+   split inside cycles too.  Both forms give identical results. */
+#define MAD_OPT_SERIAL_RANK_SWEEP 2u
+#define MAD_OPT_OVERLAP_RANK_CYCLE 4u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

@@ -14,7 +14,7 @@
 //        global colour parity, coarsening alignment, agglomeration) is testable
 //        bit-for-bit on a one-GPU machine; RCCL and LOCAL move the same bytes.
 // SOLO   measurement only: one rank of an N-rank decomposition alone on its device.
-//        Every exchange is a stream-ordered device copy of the same bytes within the
+//        Every exchange is one stream-ordered copy launch of the same bytes within the
 //        rank's own arrays (its boundary planes into its ghost planes, its slab into every
 //        slot of a gather, the allreduce a no-op), so one rank's per-cycle device time --
 //        hipGraph replay, boundary / interior launches, comm-stream overlap -- is measurable
@@ -90,6 +90,56 @@ inline std::shared_ptr<LocalGroup> local_group(uint64_t key, int nranks) {
   auto g = std::make_shared<LocalGroup>(nranks);
   groups[key] = g;
   return g;
+}
+
+// SOLO's device copies.  One grouped exchange is one kernel launch, as RCCL issues a grouped
+// ncclSend/ncclRecv (one kernel per ncclGroupEnd) -- not one copy launch per face or peer.
+// Up to 8 segments per launch (blockIdx.y), each a multiple of 4 bytes; a segment whose
+// pointers and size are 16-byte aligned moves uint4s.
+struct CopyBatch {
+  static constexpr int MAX = 8;
+  int n = 0;
+  char* dst[MAX];
+  const char* src[MAX];
+  uint64_t bytes[MAX];
+};
+
+__global__ void __launch_bounds__(256) copy_batch_k(CopyBatch b) {
+  const int q = blockIdx.y;
+  char* d = b.dst[q];
+  const char* s = b.src[q];
+  const uint64_t nb = b.bytes[q];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((((uintptr_t)d | (uintptr_t)s | nb) & 15) == 0) {
+    uint4* d4 = (uint4*)d;
+    const uint4* s4 = (const uint4*)s;
+    for (uint64_t i = t0; i < nb / 16; i += stride) d4[i] = s4[i];
+  } else {
+    uint32_t* d1 = (uint32_t*)d;
+    const uint32_t* s1 = (const uint32_t*)s;
+    for (uint64_t i = t0; i < nb / 4; i += stride) d1[i] = s1[i];
+  }
+}
+
+inline void copy_batch_flush(CopyBatch& b, hipStream_t st) {
+  if (b.n == 0) return;
+  uint64_t mx = 0;
+  for (int q = 0; q < b.n; ++q) mx = std::max(mx, b.bytes[q]);
+  const uint64_t blocks = std::min<uint64_t>(1024, std::max<uint64_t>(1, (mx / 16 + 255) / 256));
+  hipLaunchKernelGGL(copy_batch_k, dim3((unsigned)blocks, (unsigned)b.n), dim3(256), 0, st, b);
+  HIPC_CHECK(hipGetLastError());
+  b.n = 0;
+}
+
+inline void copy_batch_add(CopyBatch& b, void* dst, const void* src, uint64_t bytes, hipStream_t st) {
+  if (bytes == 0) return;
+  if (bytes % 4) throw CommError("device copy of " + std::to_string(bytes) + " bytes (not a multiple of 4)");
+  if (b.n == CopyBatch::MAX) copy_batch_flush(b, st);
+  b.dst[b.n] = (char*)dst;
+  b.src[b.n] = (const char*)src;
+  b.bytes[b.n] = bytes;
+  ++b.n;
 }
 
 class Comm {
@@ -196,11 +246,10 @@ class Comm {
       return;
     }
     if (mode_ == SOLO) {  // the same bytes, own boundary planes into own ghost planes
-      if (has_lo)
-        HIPC_CHECK(hipMemcpyAsync(base - depth * pb, base, depth * pb, hipMemcpyDeviceToDevice, s));
-      if (has_hi)
-        HIPC_CHECK(hipMemcpyAsync(base + (size_t)nz * pb, base + (size_t)(nz - depth) * pb, depth * pb,
-                                  hipMemcpyDeviceToDevice, s));
+      CopyBatch b;
+      if (has_lo) copy_batch_add(b, base - depth * pb, base, depth * pb, s);
+      if (has_hi) copy_batch_add(b, base + (size_t)nz * pb, base + (size_t)(nz - depth) * pb, depth * pb, s);
+      copy_batch_flush(b, s);
       return;
     }
     // LOCAL: publish, pull the neighbours' boundary planes, wait until all pulled
@@ -254,8 +303,10 @@ class Comm {
       return;
     }
     if (mode_ == SOLO) {  // the same bytes from this rank's own planes
-      if (has_lo) HIPC_CHECK(hipMemcpyAsync(recv_lo, send_up, d * pb, hipMemcpyDeviceToDevice, s));
-      if (has_hi) HIPC_CHECK(hipMemcpyAsync(recv_hi, send_dn, d * pb, hipMemcpyDeviceToDevice, s));
+      CopyBatch b;
+      if (has_lo) copy_batch_add(b, recv_lo, send_up, d * pb, s);
+      if (has_hi) copy_batch_add(b, recv_hi, send_dn, d * pb, s);
+      copy_batch_flush(b, s);
       return;
     }
     HIPC_CHECK(hipStreamSynchronize(s));
@@ -290,9 +341,10 @@ class Comm {
       return;
     }
     if (mode_ == SOLO) {  // the same bytes: this rank's own blocks stand in for the peers'
+      CopyBatch b;
       for (int r = 0; r < nranks_; ++r)
-        if (r != rank_ && rbytes[r])
-          HIPC_CHECK(hipMemcpyAsync(recv[r], send[r], std::min(sbytes[r], rbytes[r]), hipMemcpyDeviceToDevice, s));
+        if (r != rank_ && rbytes[r]) copy_batch_add(b, recv[r], send[r], std::min(sbytes[r], rbytes[r]), s);
+      copy_batch_flush(b, s);
       return;
     }
     // LOCAL: publish the send table, pull every peer's block addressed to this rank
@@ -360,8 +412,9 @@ class Comm {
       return;
     }
     if (mode_ == SOLO) {  // the same bytes: the own slab into every rank's slot
-      for (int r = 0; r < nranks_; ++r)
-        HIPC_CHECK(hipMemcpyAsync((char*)full + r * bytes, slab, bytes, hipMemcpyDeviceToDevice, s));
+      CopyBatch b;
+      for (int r = 0; r < nranks_; ++r) copy_batch_add(b, (char*)full + r * bytes, slab, bytes, s);
+      copy_batch_flush(b, s);
       return;
     }
     HIPC_CHECK(hipStreamSynchronize(s));

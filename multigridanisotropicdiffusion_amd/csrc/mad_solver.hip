@@ -693,7 +693,12 @@ class Solver final : public SolverBase {
     const LevelData<T>& L = lv_[l];
     if (!(c_->comm.active() && c_->geom[l].distributed && L.g.nz >= 3 * boundary_planes()))
       return false;
+    if (c_->d.options & MAD_OPT_SERIAL_RANK_SWEEP) return false;
     if (c_->d.gs_kernel != 0) return true;
+    // inside a V-cycle / FMG one stream: the cycle is replayed as one hipGraph, and a graph
+    // with a communication-stream branch launches every one of its ~130 nodes ~2 us slower
+    // (8-rank SOLO cycle 1.81 -> 1.52 ms serial, profiles/r03_rank_serial_ab.md)
+    if (in_cycle_ > 0 && !(c_->d.options & MAD_OPT_OVERLAP_RANK_CYCLE)) return false;
     int tiles = 0, nchunks = 0;
     fused_shape(L, &tiles, &nchunks);
     return 2 * tiles >= 128;
@@ -1113,7 +1118,16 @@ class Solver final : public SolverBase {
   }
 
   // ------------------------------------------------------------- cycles
+  // marks the sweeps issued inside a V-cycle / FMG (sweep_overlap: serial rank sweeps)
+  struct CycleScope {
+    int& d;
+    explicit CycleScope(int& depth) : d(depth) { ++d; }
+    ~CycleScope() { --d; }
+  };
+  int in_cycle_ = 0;
+
   void vcycle_rec(int l) {
+    CycleScope cs(in_cycle_);
     const int nl = c_->nlev;
     if (l == nl - 1) {  // MAD.hxx:356-371
       coarse_solve();
@@ -1177,6 +1191,7 @@ class Solver final : public SolverBase {
 
   // MAD.hxx:300-338 (rhs already in b[l])
   void fmg_rec(int l) {
+    CycleScope cs(in_cycle_);
     const int nl = c_->nlev;
     if (l == nl - 1) {
       fill(l, MAD_X, 0.0);
@@ -2290,7 +2305,8 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             "bad rank / nranks");
     REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
-    REQUIRE((d->options & ~MAD_OPT_EAGER_RANK_VCYCLE) == 0, MAD_ERR_INVALID, "unknown option bits");
+    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_SERIAL_RANK_SWEEP |
+                              MAD_OPT_OVERLAP_RANK_CYCLE)) == 0, MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");

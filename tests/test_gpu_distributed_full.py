@@ -3,8 +3,9 @@ ranks, C5 1024 x 1024 x 512 at 8 ranks), rehearsed on one GPU with the in-proces
 transport (ranks as host threads; the RCCL path moves the same planes).
 
 Two level-0 sweeps and one V-cycle on the rank slabs must equal the single-rank run
-BIT for bit, with the default (fused, boundary + interior overlapped) sweep on the
-64-plane slabs of the 8-rank C4 split.  Inputs are generated on the device from
+BIT for bit, with the default fused rank sweeps on the 64-plane slabs of the 8-rank C4
+split: mad_smooth's split form (boundary + interior launches, exchange overlapped) and the
+V-cycle's serial form (one launch, then the exchange).  Inputs are generated on the device from
 global coordinates (mad_bench_synth_tensor / mad_bench_synth_level), so every rank
 builds the same operator the single-rank run builds.
 

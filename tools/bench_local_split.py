@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def solo(ns, msp=0, gsk=0):
+def solo(ns, msp=0, gsk=0, opts=0):
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     S, sweeps, vcyc = 512, 20, 10
@@ -32,11 +32,11 @@ def solo(ns, msp=0, gsk=0):
     for n in ns:
         r = n // 2
         z0, z1 = D.slabs((S, S, S), n)[r]
-        out = {"ranks": n, "rank": r, "slab": [z1 - z0, S, S], "min_slab_planes": msp, "gs_kernel": gsk,
+        out = {"ranks": n, "rank": r, "slab": [z1 - z0, S, S], "min_slab_planes": msp, "gs_kernel": gsk, "options": opts,
                "distributed_levels": sum(p["distributed"] for p in D.plan((S, S, S), n, r, msp))}
         for cyc, key in ((M.SMOOTHER, "sweep"), (M.VCYCLE, "vcycle")):
             kw = dict(nranks=n, rank=r, global_shape=(S, S, S), min_slab_planes=msp) if n > 1 else {}
-            s = M.Solver((z1 - z0, S, S), time_step=0.1, cycle=cyc, gs_kernel=gsk, **kw)
+            s = M.Solver((z1 - z0, S, S), time_step=0.1, cycle=cyc, gs_kernel=gsk, options=opts, **kw)
             if n > 1:
                 s.comm_init_solo()
             s.synth_tensor(kind=0, seed=4)
@@ -74,8 +74,13 @@ def main():
         i = args.index("--gs-kernel")
         gsk = int(args[i + 1])
         del args[i:i + 2]
+    opts = 0
+    if "--options" in args:  # mad_desc.options (MAD_OPT_* bits)
+        i = args.index("--options")
+        opts = int(args[i + 1])
+        del args[i:i + 2]
     if args and args[0] == "--solo":
-        return solo([int(v) for v in (args[1:] or ["1", "2", "4", "8"])], msp, gsk)
+        return solo([int(v) for v in (args[1:] or ["1", "2", "4", "8"])], msp, gsk, opts)
     S, sweeps, vcyc = 512, 20, 3
     for n in [int(v) for v in (args or ["1", "2", "4", "8"])]:
         bar = threading.Barrier(n)
