@@ -135,14 +135,14 @@ typedef struct mad_desc {
 /* mad_desc.options: MAD_OPT_EAGER_RANK_VCYCLE keeps a multi-rank V-cycle eager instead of
    replaying its captured hipGraph (the reference of the graph-replay parity test) */
 #define MAD_OPT_EAGER_RANK_VCYCLE 1u
-/* Rank-slab fused sweeps come in two forms: split (boundary chunks, then the halo exchange on a
-   communication stream beside the interior launch) and serial (one launch, then the exchange on
-   the solver's stream).  By default mad_smooth uses the split and V-cycles / FMG the serial form
-   (a second stream inside the captured cycle graph slows every node's launch).
-   MAD_OPT_SERIAL_RANK_SWEEP makes every rank sweep serial; MAD_OPT_OVERLAP_RANK_CYCLE keeps the
-   split inside cycles too.  Both forms give identical results. */
-#define MAD_OPT_SERIAL_RANK_SWEEP 2u
-#define MAD_OPT_OVERLAP_RANK_CYCLE 4u
+/* MAD_OPT_OVERLAP_RANK_SWEEP: a rank slab's fused sweep runs split -- its two boundary chunks first,
+   then the halo exchange on a communication stream beside the interior launch -- instead of the
+   default serial form (one launch, then the exchange on the solver's stream).  Identical results.
+   The sweep fills every CU, so an exchange kernel released beside it either waits for the sweep
+   or delays the sweep's workgroups on the CUs it takes; the split also costs a short boundary
+   launch and, in a captured V-cycle graph, a second stream that slows every node's launch
+   (DESIGN.md "Multi-GPU"). */
+#define MAD_OPT_OVERLAP_RANK_SWEEP 2u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

@@ -31,8 +31,7 @@ TENSOR_AUTO, TENSOR_ISOTROPIC, TENSOR_DIAGONAL, TENSOR_FULL = range(4)
 X, B, R = 0, 1, 2
 # mad_desc.options / mad_ved_desc.options
 OPT_EAGER_RANK_VCYCLE = 1
-OPT_SERIAL_RANK_SWEEP = 2
-OPT_OVERLAP_RANK_CYCLE = 4
+OPT_OVERLAP_RANK_SWEEP = 2
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (

@@ -683,36 +683,35 @@ class Solver final : public SolverBase {
   }
 
   // Does the fused sweep of rank-slab level l overlap its halo exchange (boundary chunks
-  // first, the exchange beside the interior launch, or gs_kernel 4's single launch)?  The
-  // default form (gs_kernel 0) only where the boundary launch keeps half the chip busy
-  // (2 chunks x tiles per plane >= 128 workgroups): on smaller levels the split's short,
-  // under-filled boundary launch costs more than the exchange it hides (a 256^2-plane level
-  // at 2 ranks: 56 + 102 us per sweep split, profiles/r02_rank_vcycle.md), so they sweep in
-  // one launch and exchange afterwards.
+  // first, the exchange beside the interior launch, or gs_kernel 4's single launch)?  Not by
+  // default: one launch, then the exchange on the solver's stream.  With
+  // MAD_OPT_OVERLAP_RANK_SWEEP, gs_kernel 0 splits only where the boundary launch keeps half
+  // the chip busy (2 chunks x tiles per plane >= 128 workgroups): on smaller levels the
+  // split's short, under-filled boundary launch costs more than the exchange it hides (a
+  // 256^2-plane level at 2 ranks: 56 + 102 us per sweep split, profiles/r02_rank_vcycle.md).
   bool sweep_overlap(int l) const {
     const LevelData<T>& L = lv_[l];
     if (!(c_->comm.active() && c_->geom[l].distributed && L.g.nz >= 3 * boundary_planes()))
       return false;
-    if (c_->d.options & MAD_OPT_SERIAL_RANK_SWEEP) return false;
+    if (c_->d.gs_kernel == 4) return true;  // the single-launch form exchanges mid-sweep
+    // default serial (profiles/r03_rank_serial_ab.md: per-rank sweep 0.195 vs 0.235 ms and
+    // V-cycle 1.52 vs 1.81 ms at 8 ranks; a cycle graph with a communication-stream branch
+    // launches every one of its ~130 nodes ~2 us slower)
+    if (!(c_->d.options & MAD_OPT_OVERLAP_RANK_SWEEP)) return false;
     if (c_->d.gs_kernel != 0) return true;
-    // inside a V-cycle / FMG one stream: the cycle is replayed as one hipGraph, and a graph
-    // with a communication-stream branch launches every one of its ~130 nodes ~2 us slower
-    // (8-rank SOLO cycle 1.81 -> 1.52 ms serial, profiles/r03_rank_serial_ab.md)
-    if (in_cycle_ > 0 && !(c_->d.options & MAD_OPT_OVERLAP_RANK_CYCLE)) return false;
     int tiles = 0, nchunks = 0;
     fused_shape(L, &tiles, &nchunks);
     return 2 * tiles >= 128;
   }
 
-  // one fused GS sweep x -> t, then swap (gs_fused_k)
-  // One fused GS sweep x -> t, then swap.  On a rank slab the halo exchange of the NEW
-  // x is overlapped with the sweep: the two boundary chunks (which produce the planes
-  // the neighbours need) run first, the exchange of their output then runs on the
-  // communication stream while the interior chunks sweep, and the next consumer of
-  // x's ghost planes waits for it (halo()).  Slabs thinner than 3 boundary chunks
-  // sweep in one launch and exchange afterwards.  gs_kernel 4 makes the boundary and
-  // interior launches one launch instead (part 3: edge chunks signal their finished
-  // edge planes to the communication stream, which waits on the counters).
+  // One fused GS sweep x -> t, then swap.  On a rank slab the next consumer of x's ghost
+  // planes exchanges them (halo()), by default right after this one launch.  The overlapped
+  // form (sweep_overlap): the two boundary chunks (which produce the planes the neighbours
+  // need) run first, the exchange of their output then runs on the communication stream
+  // while the interior chunks sweep, and the next consumer waits for it.  gs_kernel 4
+  // makes the boundary and interior launches one launch instead (part 3: edge chunks
+  // signal their finished edge planes to the communication stream, which waits on the
+  // counters).
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
     halo(l, L.x, GHOST);
@@ -1118,16 +1117,7 @@ class Solver final : public SolverBase {
   }
 
   // ------------------------------------------------------------- cycles
-  // marks the sweeps issued inside a V-cycle / FMG (sweep_overlap: serial rank sweeps)
-  struct CycleScope {
-    int& d;
-    explicit CycleScope(int& depth) : d(depth) { ++d; }
-    ~CycleScope() { --d; }
-  };
-  int in_cycle_ = 0;
-
   void vcycle_rec(int l) {
-    CycleScope cs(in_cycle_);
     const int nl = c_->nlev;
     if (l == nl - 1) {  // MAD.hxx:356-371
       coarse_solve();
@@ -1191,7 +1181,6 @@ class Solver final : public SolverBase {
 
   // MAD.hxx:300-338 (rhs already in b[l])
   void fmg_rec(int l) {
-    CycleScope cs(in_cycle_);
     const int nl = c_->nlev;
     if (l == nl - 1) {
       fill(l, MAD_X, 0.0);
@@ -2305,8 +2294,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             "bad rank / nranks");
     REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
-    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_SERIAL_RANK_SWEEP |
-                              MAD_OPT_OVERLAP_RANK_CYCLE)) == 0, MAD_ERR_INVALID, "unknown option bits");
+    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP)) == 0, MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");

@@ -37,9 +37,9 @@ def _multi(nranks, fn, T, **kw):
                                                               (0, 3, 2, 2)])
 def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle, options):
     """cycle 2 (SMOOTHER): level-0 records carry b (sync_brec on ghost planes).  gs_kernel 3 forces
-    the fused sweep on these small levels in its split rank form (boundary chunks, exchange beside
-    the interior launch); options 2 (MAD_OPT_SERIAL_RANK_SWEEP) in its serial form (one launch, then
-    the exchange) -- the form V-cycles use on large levels by default."""
+    the fused sweep on these small levels, in its default serial rank form (one launch, then the
+    exchange) or with options 2 (MAD_OPT_OVERLAP_RANK_SWEEP) in the split form (boundary chunks,
+    exchange beside the interior launch)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     T = synth.random_spd(SHAPE, seed=3)
@@ -214,21 +214,21 @@ def test_solo_transport_times_one_rank():
         s.close()
 
 
-@pytest.mark.parametrize("cycle,gs_kernel,serial", [(0, 0, 0), (2, 0, 0), (0, 3, 1), (0, 3, 0)])
-def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, serial):
+@pytest.mark.parametrize("cycle,gs_kernel,overlap", [(0, 0, 0), (2, 0, 0), (0, 3, 0), (0, 3, 1)])
+def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     """The multi-rank V-cycle replays a captured hipGraph on RCCL / SOLO ranks (host bookkeeping
     of which ghost planes are current decides what the graph re-exchanges).  On the SOLO
     transport (deterministic: every exchange a device copy) the same sequence -- sweeps,
     several V-cycles, an odd sweep count in between (the ping-pong parity flips), more
     V-cycles -- equals the eager execution (mad_desc.options MAD_OPT_EAGER_RANK_VCYCLE) bit for
-    bit on every level's x and b; gs_kernel 3 puts the fused rank sweep into the graph, split
-    (the communication-stream branch) or serial (MAD_OPT_SERIAL_RANK_SWEEP)."""
+    bit on every level's x and b; gs_kernel 3 puts the fused rank sweep into the graph, serial
+    (the default) or split (MAD_OPT_OVERLAP_RANK_SWEEP: a communication-stream branch)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     shape = (128, 64, 64)
     z0, z1 = D.slabs(shape, 4)[2]
     out = {}
-    base = M.capi.OPT_SERIAL_RANK_SWEEP if serial else 0
+    base = M.capi.OPT_OVERLAP_RANK_SWEEP if overlap else 0
     for opt in (0, M.capi.OPT_EAGER_RANK_VCYCLE):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
                      global_shape=shape, options=opt | base, gs_kernel=gs_kernel)

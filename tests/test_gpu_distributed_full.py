@@ -3,9 +3,9 @@ ranks, C5 1024 x 1024 x 512 at 8 ranks), rehearsed on one GPU with the in-proces
 transport (ranks as host threads; the RCCL path moves the same planes).
 
 Two level-0 sweeps and one V-cycle on the rank slabs must equal the single-rank run
-BIT for bit, with the default fused rank sweeps on the 64-plane slabs of the 8-rank C4
-split: mad_smooth's split form (boundary + interior launches, exchange overlapped) and the
-V-cycle's serial form (one launch, then the exchange).  Inputs are generated on the device from
+BIT for bit, with the default fused rank sweep (one launch, then the exchange) on the
+64-plane slabs of the 8-rank C4 split, and with the split form (boundary + interior
+launches, exchange overlapped: MAD_OPT_OVERLAP_RANK_SWEEP) on the 8-rank SMOOTHER case.  Inputs are generated on the device from
 global coordinates (mad_bench_synth_tensor / mad_bench_synth_level), so every rank
 builds the same operator the single-rank run builds.
 
@@ -40,7 +40,8 @@ def _drive(s, M):
 def test_full_size_slabs_bitwise(gshape, nranks, cycle):
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
-    kw = dict(time_step=0.1, precision=M.FP32, cycle=cycle, gs_kernel=0)
+    opts = M.capi.OPT_OVERLAP_RANK_SWEEP if cycle == 2 else 0
+    kw = dict(time_step=0.1, precision=M.FP32, cycle=cycle, gs_kernel=0, options=opts)
     s = M.Solver(gshape, **kw)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
