@@ -293,6 +293,13 @@ int mad_comm_init_local(mad_ctx *ctx, uint64_t group);
  * graph replay, boundary + interior launches, communication-stream overlap -- can be
  * timed on a one-GPU machine.  The values it computes are not the solution. */
 int mad_comm_init_solo(mad_ctx *ctx);
+/* Measurement only, as mad_comm_init_solo, but every exchange goes through RCCL: a single-rank
+ * communicator on ctx's device, each grouped exchange a group of ncclSend / ncclRecv pairs to
+ * itself moving the same bytes as mad_comm_init_solo's copies, the norm a one-rank
+ * ncclAllReduce.  One rank's per-sweep / per-V-cycle time then includes RCCL's kernels, their
+ * launch latency and their capture into the V-cycle graph (not the xGMI transfer time).
+ * Results equal mad_comm_init_solo's bit for bit. */
+int mad_comm_init_rccl_solo(mad_ctx *ctx);
 /* Transport self-test on one GPU: a single-rank RCCL communicator runs the halo
  * exchange (grouped ncclSend/ncclRecv, both neighbours = this rank), the fp64
  * allreduce and the slab allgather the solver uses, on `device`, first eagerly and

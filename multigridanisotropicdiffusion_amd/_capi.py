@@ -45,6 +45,7 @@ EXPORTS = (
     "mad_interpolate", "mad_prolongate_add", "mad_coarse_solve", "mad_vcycle", "mad_fmg",
     "mad_synchronize", "mad_bench_smooth", "mad_bench_launch_times", "mad_smooth_kernel_name", "mad_bench_vcycle", "mad_bench_synth_tensor",
     "mad_bench_synth_level", "mad_comm_unique_id", "mad_comm_init", "mad_comm_init_local", "mad_comm_init_solo",
+    "mad_comm_init_rccl_solo",
     "mad_comm_selftest", "mad_slab_range", "mad_comm_allreduce_host", "mad_comm_version",
     # include/mad_ved.h
     "mad_ved_desc_init", "mad_ved_create", "mad_ved_destroy", "mad_ved_last_error",
@@ -220,6 +221,7 @@ def load():
         "mad_comm_init": ([vp, vp], i32),
         "mad_comm_init_local": ([vp, ctypes.c_uint64], i32),
         "mad_comm_init_solo": ([vp], i32),
+        "mad_comm_init_rccl_solo": ([vp], i32),
         "mad_comm_selftest": ([i32, dp], i32),
         "mad_slab_range": ([i64, i32, i32, i32, i64p, i64p], i32),
         "mad_comm_allreduce_host": ([vp, dp, u32, i32], i32),

@@ -19,6 +19,10 @@
 //        slot of a gather, the allreduce a no-op), so one rank's per-cycle device time --
 //        hipGraph replay, boundary / interior launches, comm-stream overlap -- is measurable
 //        on a one-GPU box.  The numbers it computes are not the decomposition's results.
+//        RCCL-SOLO (init_rccl_self): the same stand-in exchanges through RCCL -- a single-rank
+//        communicator, every grouped exchange ncclSend / ncclRecv to itself, the allreduce a
+//        one-rank ncclAllReduce -- so the per-rank timing includes RCCL's kernels, their
+//        launch latency and their capture into the V-cycle graph (not xGMI bandwidth).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -189,6 +193,18 @@ class Comm {
     rank_ = rank;
   }
 
+  // RCCL-SOLO: a single-rank communicator standing in for rank `rank` of `nranks`
+  void init_rccl_self(int nranks, int rank, int device) {
+    destroy();
+    if (nranks <= 1) return;
+    ncclUniqueId id;
+    NCCL_CHECK(ncclGetUniqueId(&id));
+    init_rccl(&id, 1, 0, device);
+    self_ = true;
+    nranks_ = nranks;
+    rank_ = rank;
+  }
+
   void init_local(uint64_t key, int nranks, int rank) {
     destroy();
     if (nranks <= 1) return;
@@ -211,15 +227,36 @@ class Comm {
     if (comm_) (void)ncclCommDestroy(comm_);
     comm_ = nullptr;
     group_.reset();
+    self_ = false;
     mode_ = NONE;
     nranks_ = 1;
     rank_ = 0;
   }
 
   bool active() const { return mode_ != NONE && nranks_ > 1; }
+  bool self() const { return self_; }
+  // RCCL peer of neighbour rank q (RCCL-SOLO: every peer is this process's only rank)
+  int peer(int q) const { return self_ ? 0 : (q + nranks_) % nranks_; }
   Mode mode() const { return mode_; }
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
+
+  // RCCL-SOLO: the SOLO copies (dst <- src, bytes a multiple of 4) as one group of ncclSend /
+  // ncclRecv pairs to this process's only rank (pairs to one peer match in posting order)
+  struct SelfPair {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  void self_exchange(const std::vector<SelfPair>& pairs, hipStream_t s) {
+    NCCL_CHECK(ncclGroupStart());
+    for (const SelfPair& q : pairs) {
+      if (!q.bytes) continue;
+      NCCL_CHECK(ncclSend(q.src, q.bytes / 4, ncclFloat, 0, comm_, s));
+      NCCL_CHECK(ncclRecv(q.dst, q.bytes / 4, ncclFloat, 0, comm_, s));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+  }
 
   // a: base pointer of local plane 0; planes -depth..-1 and nz..nz+depth-1 are ghosts.
   // The first / last `depth` owned planes go to rank -+ 1.
@@ -227,12 +264,19 @@ class Comm {
                        size_t esz, bool is_double, hipStream_t s) {
     char* base = (char*)a;
     const size_t pb = (size_t)plane * esz;
+    if (mode_ == RCCL && self_) {  // SOLO's bytes: own boundary planes into own ghost planes
+      std::vector<SelfPair> q;
+      if (has_lo) q.push_back({base - depth * pb, base, depth * pb});
+      if (has_hi) q.push_back({base + (size_t)nz * pb, base + (size_t)(nz - depth) * pb, depth * pb});
+      self_exchange(q, s);
+      return;
+    }
     if (mode_ == RCCL) {
       const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
       const size_t cnt = (size_t)plane * depth;
       // neighbour ranks (has_lo / has_hi are false at the global ends; the modulo only
       // matters for the single-rank self-test, where both neighbours are this rank)
-      const int lo = (rank_ - 1 + nranks_) % nranks_, hi = (rank_ + 1) % nranks_;
+      const int lo = peer(rank_ - 1), hi = peer(rank_ + 1);
       NCCL_CHECK(ncclGroupStart());
       if (has_lo) {
         NCCL_CHECK(ncclSend(base, cnt, dt, lo, comm_, s));
@@ -286,10 +330,17 @@ class Comm {
     char* recv_hi = base + (size_t)(nz + D) * pb;
     char* send_up = base + (ptrdiff_t)(nz - D - d) * (ptrdiff_t)pb;
     char* recv_lo = base - (ptrdiff_t)(D + d) * (ptrdiff_t)pb;
+    if (mode_ == RCCL && self_) {  // SOLO's bytes
+      std::vector<SelfPair> q;
+      if (has_lo) q.push_back({recv_lo, send_up, d * pb});
+      if (has_hi) q.push_back({recv_hi, send_dn, d * pb});
+      self_exchange(q, s);
+      return;
+    }
     if (mode_ == RCCL) {
       const ncclDataType_t dt = is_double ? ncclDouble : ncclFloat;
       const size_t cnt = (size_t)plane * d;
-      const int lo = (rank_ - 1 + nranks_) % nranks_, hi = (rank_ + 1) % nranks_;
+      const int lo = peer(rank_ - 1), hi = peer(rank_ + 1);
       NCCL_CHECK(ncclGroupStart());
       if (has_lo) {
         NCCL_CHECK(ncclSend(send_dn, cnt, dt, lo, comm_, s));
@@ -330,6 +381,13 @@ class Comm {
   // counts are multiples of 4 (fp32 / fp64 volumes).
   void exchange_blocks(const std::vector<const void*>& send, const std::vector<size_t>& sbytes,
                        const std::vector<void*>& recv, const std::vector<size_t>& rbytes, hipStream_t s) {
+    if (mode_ == RCCL && self_) {  // the own blocks stand in for the peers' (as SOLO)
+      std::vector<SelfPair> q;
+      for (int r = 0; r < nranks_; ++r)
+        if (r != rank_ && rbytes[r]) q.push_back({recv[r], send[r], std::min(sbytes[r], rbytes[r])});
+      self_exchange(q, s);
+      return;
+    }
     if (mode_ == RCCL) {
       NCCL_CHECK(ncclGroupStart());
       for (int r = 0; r < nranks_; ++r) {
@@ -407,6 +465,12 @@ class Comm {
   void allgather_slabs(const void* slab, void* full, int64_t plane, int64_t nz_global, size_t esz,
                        hipStream_t s) {
     const size_t bytes = (size_t)plane * (size_t)(nz_global / nranks_) * esz;
+    if (mode_ == RCCL && self_) {  // the own slab into every rank's slot (as SOLO)
+      std::vector<SelfPair> q;
+      for (int r = 0; r < nranks_; ++r) q.push_back({(char*)full + r * bytes, slab, bytes});
+      self_exchange(q, s);
+      return;
+    }
     if (mode_ == RCCL) {
       NCCL_CHECK(ncclAllGather(slab, full, bytes / 4, ncclFloat, comm_, s));
       return;
@@ -433,6 +497,7 @@ class Comm {
   std::shared_ptr<LocalGroup> group_;
   int nranks_ = 1;
   int rank_ = 0;
+  bool self_ = false;
 };
 
 }  // namespace mad

@@ -1280,7 +1280,8 @@ __global__ void __launch_bounds__(CX * CY) restrict3_k(const T* __restrict__ fin
 // in the ring, as resid3_k), the residuals go to an LDS tile, and restrict3_k's x-y
 // taps, z window and emission follow.  Residual arithmetic = resid3_k's, restriction
 // arithmetic = restrict3_k's, so b_c is bit-identical to residual + restriction.  With zx
-// set, the coarse x is zeroed on the way (the descent's fill, MAD.hxx:415-416).
+// set, the coarse x is zeroed on the way (the descent's fill, MAD.hxx:415-416), on a rank
+// slab with its ghost planes.
 // Rank slabs: the coarse planes' taps are taken in global indices (coarse zoff, global coarse
 // nz `ncz`) and shifted to local fine planes by fzs (the fine zoff); taps past the slab
 // residualise the fine ghost planes (u, b and records current there: >= 2 ghost planes), the
@@ -1459,7 +1460,20 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
         if (ok) {
           const int64_t o = I + gc.sy * J + gc.sz * (int64_t)K;
           coarse[o] = v;
-          if (zx) zx[o] = T(0);
+          if (zx) {
+            zx[o] = T(0);
+            // a rank slab's edge planes zero the GHOST ghost planes beyond them too: every rank
+            // zeroes its own planes, so the neighbours' planes they stand for are zeros (no
+            // exchange of the zeroed coarse x)
+            if (K == 0 && gc.zlo_ghost) {
+#pragma unroll
+              for (int g = 1; g <= GHOST; ++g) zx[o - gc.sz * (int64_t)g] = T(0);
+            }
+            if (K == gc.nz - 1 && gc.zhi_ghost) {
+#pragma unroll
+              for (int g = 1; g <= GHOST; ++g) zx[o + gc.sz * (int64_t)g] = T(0);
+            }
+          }
         }
         ++K;
         if (K < K1) ztaps(K);

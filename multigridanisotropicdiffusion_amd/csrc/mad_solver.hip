@@ -1018,7 +1018,8 @@ class Solver final : public SolverBase {
     sync_brec(l);
     C.b_halo_ok = C.brec_ok = false;
     T* zx = zero_x ? C.x : nullptr;
-    if (zero_x) x_changed(l + 1);
+    // the kernel zeroes a rank slab's coarse x ghost planes too (the neighbours' zeros)
+    if (zero_x) C.x_halo_ok = dist;
     // 32 x 8 coarse tiles in 512-thread blocks, two per CU (one block's barriers overlap the
     // other's loads), ~1024 blocks: 1.133 vs 1.177 ms per 512^3 launch with 1024-thread blocks
     // (profiles/r01_rr_nt_prof.log, r01_rr_blocks_prof.log)
@@ -2827,6 +2828,17 @@ int mad_comm_init_solo(mad_ctx* c) {
     REQUIRE(!c->setup_done, MAD_ERR_STATE, "mad_comm_init_solo must precede mad_setup");
     use_device(c);
     c->comm.init_solo(c->d.nranks, c->d.rank);
+  });
+}
+
+int mad_comm_init_rccl_solo(mad_ctx* c) {
+  if (!c) return MAD_ERR_INVALID;
+  return guarded(c, [&] {
+    REQUIRE(!c->setup_done, MAD_ERR_STATE, "mad_comm_init_rccl_solo must precede mad_setup");
+    use_device(c);
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    c->comm.init_rccl_self(c->d.nranks, c->d.rank, dev);
   });
 }
 

@@ -6,6 +6,7 @@ classes live in ``filters.py``.  numpy arrays use (z, y, x) / (y, x) order;
 the C ABI takes sizes and spacings x first, as ITK does.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -162,6 +163,14 @@ class Solver:
         """Measurement only (mad_comm_init_solo): this rank alone on its device, every
         exchange a device copy of the same bytes; timings, not results."""
         self._check(self._L.mad_comm_init_solo(self._ctx))
+
+    def comm_init_rccl_solo(self):
+        """Measurement only (mad_comm_init_rccl_solo): as comm_init_solo, every exchange through a
+        single-rank RCCL communicator (ncclSend / ncclRecv to itself, the same bytes): RCCL's
+        kernels and launch latency in the per-rank timing."""
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")  # one node: bootstrap on loopback
+        self._check(self._L.mad_comm_init_rccl_solo(self._ctx))
+
     def setup(self):
         self._check(self._L.mad_setup(self._ctx))
 

@@ -251,3 +251,39 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
         assert np.isfinite(xa).all()
         np.testing.assert_array_equal(xa, xb, err_msg=f"x, level {l}")
         np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")
+
+
+@pytest.mark.parametrize("cycle,gs_kernel", [(0, 0), (0, 3), (2, 3)])
+def test_rccl_solo_equals_solo(cycle, gs_kernel):
+    """mad_comm_init_rccl_solo moves SOLO's bytes through RCCL (a single-rank communicator, every
+    grouped exchange ncclSend / ncclRecv pairs to itself, inside the captured V-cycle graph too):
+    the same sequence -- partitioned setup (hop-by-hop tensor ghost planes), sweeps, graph-replayed
+    V-cycles, an odd sweep count, more V-cycles -- gives SOLO's result bit for bit on every level."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (128, 64, 64)
+    z0, z1 = D.slabs(shape, 4)[2]
+    out = {}
+    for mode in ("solo", "rccl"):
+        s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
+                     global_shape=shape, gs_kernel=gs_kernel)
+        if mode == "solo":
+            s.comm_init_solo()
+        else:
+            s.comm_init_rccl_solo()
+        s.synth_tensor(kind=0, seed=9)
+        s.setup()
+        s.synth_level(0, M.capi.B, 3)
+        s.synth_level(0, M.capi.X, 4)
+        s.smooth(0, 2)
+        for _ in range(3):
+            s.vcycle()
+        s.smooth(0, 1)
+        for _ in range(2):
+            s.vcycle()
+        out[mode] = [(s.download(l, M.capi.X), s.download(l, M.capi.B)) for l in range(s.num_levels)]
+        s.close()
+    for l, ((xa, ba), (xb, bb)) in enumerate(zip(out["solo"], out["rccl"])):
+        assert np.isfinite(xa).all()
+        np.testing.assert_array_equal(xa, xb, err_msg=f"x, level {l}")
+        np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")

@@ -20,6 +20,8 @@ def main():
                    help="> 1: one interior rank (ranks // 2) of that z-slab decomposition alone "
                         "on the device (mad_comm_init_solo; timings, not results)")
     p.add_argument("--options", type=int, default=0, help="mad_desc.options (MAD_OPT_* bits)")
+    p.add_argument("--rccl", action="store_true",
+                   help="with --ranks: exchanges through RCCL (mad_comm_init_rccl_solo)")
     p.add_argument("--sweeps", type=int, default=0,
                    help="> 0: time that many level-0 sweeps instead of V-cycles")
     a = p.parse_args()
@@ -32,7 +34,10 @@ def main():
         z0, z1 = D.slabs((S, S, S), a.ranks)[r]
         s = M.Solver((z1 - z0, S, S), time_step=0.1, precision=M.FP32, cycle=cyc, nranks=a.ranks,
                      rank=r, global_shape=(S, S, S), options=a.options)
-        s.comm_init_solo()
+        if a.rccl:
+            s.comm_init_rccl_solo()
+        else:
+            s.comm_init_solo()
     else:
         s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32, cycle=cyc)
     s.synth_tensor(kind=0, seed=4)
