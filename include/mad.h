@@ -78,8 +78,10 @@ typedef enum mad_precision {
   MAD_FP32 = 0, MAD_FP64 = 1, MAD_FP32_REFINE = 2, MAD_PRECISION_AUTO = 3
 } mad_precision;
 #define MAD_FP32_TOLERANCE_FLOOR 1e-6
-/* default mad_desc.min_slab_planes (measured: profiles/r03_agglomeration.md) */
+/* defaults of mad_desc.min_slab_planes / min_slab_voxels (measured: profiles/r03_agglomeration.md,
+   profiles/r03_rank_serial_ab.md) */
 #define MAD_MIN_SLAB_PLANES 4
+#define MAD_MIN_SLAB_VOXELS 131072
 
 typedef enum mad_tensor_kind {
   MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */
@@ -126,10 +128,13 @@ typedef struct mad_desc {
                                     bit-identical */
   uint32_t options;              /* MAD_OPT_* bits, default 0 */
   int32_t min_slab_planes;       /* z-slab decomposition: a coarse level stays distributed while
-                                    every rank keeps >= this many planes of it (and >= 32x32x8
-                                    voxels); the first level below is replicated on every rank
+                                    every rank keeps >= this many planes of it and >= min_slab_voxels
+                                    voxels; the first level below is replicated on every rank
                                     (agglomeration).  0 = default (MAD_MIN_SLAB_PLANES) */
-  int32_t reserved[6];
+  int32_t min_slab_voxels;       /* 0 = default (MAD_MIN_SLAB_VOXELS): below ~128 K voxels per rank a
+                                    level's exchanges (one RCCL round trip per sweep) cost more than
+                                    sweeping the whole level on every rank */
+  int32_t reserved[5];
 } mad_desc;
 
 /* mad_desc.options: MAD_OPT_EAGER_RANK_VCYCLE keeps a multi-rank V-cycle eager instead of

@@ -81,7 +81,8 @@ class MadDesc(ctypes.Structure):
         ("gs_kernel", ctypes.c_int32),
         ("options", ctypes.c_uint32),
         ("min_slab_planes", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("min_slab_voxels", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 

@@ -2187,11 +2187,11 @@ std::vector<LevelGeom> plan_geometry(const mad_desc& d) {
     G.z1 = G.n[2];
     G.distributed = false;
   }
-  // z-slab decomposition: level l is distributed while every rank keeps >= 4
-  // planes, nz divides evenly and every coarsening down to l halves z exactly
-  // (cell-centred), so fine planes 2K, 2K+1 and coarse plane K share a rank.
-  // The first level below that (or below ~32^2x8 voxels per rank) and all
-  // coarser ones are replicated on every rank (agglomeration).
+  // z-slab decomposition: level l is distributed while every rank keeps >= min_slab_planes
+  // planes and >= min_slab_voxels voxels (level 0: >= 4 planes), nz divides evenly and every
+  // coarsening down to l halves z exactly (cell-centred), so fine planes 2K, 2K+1 and coarse
+  // plane K share a rank.  The first level below that and all coarser ones are replicated on
+  // every rank (agglomeration).
   if (d.nranks > 1) {
     REQUIRE(dim == 3, MAD_ERR_UNSUPPORTED, "z-slab decomposition needs a 3D image");
     const int P = d.nranks;
@@ -2199,14 +2199,15 @@ std::vector<LevelGeom> plan_geometry(const mad_desc& d) {
             "z size must split into >= 4 planes per rank");
     REQUIRE(nlev >= 2, MAD_ERR_UNSUPPORTED, "multi-GPU needs at least two levels");
     const int64_t minp = std::max(4, d.min_slab_planes > 0 ? d.min_slab_planes : MAD_MIN_SLAB_PLANES);
+    const int64_t minv = d.min_slab_voxels > 0 ? d.min_slab_voxels : MAD_MIN_SLAB_VOXELS;
     int ld = 0;
     for (int l = 0; l < nlev - 1; ++l) {
       const LevelGeom& G = geom[l];
       bool ok = (G.n[2] % P == 0) && (G.n[2] / P >= (l == 0 ? 4 : minp));
+      if (l > 0) ok = ok && G.n[0] * G.n[1] * (G.n[2] / P) >= minv;
       for (int q = 1; q <= l; ++q) ok = ok && (geom[q].cent[2] == 1);
       if (!ok) break;
       ld = l;
-      if (G.n[0] * G.n[1] * (G.n[2] / P) < 32 * 32 * 8) break;
     }
     for (int l = 0; l <= ld; ++l) {
       LevelGeom& G = geom[l];
@@ -2297,6 +2298,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
     REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP)) == 0, MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
+    REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");
     c->d = *d;

@@ -29,10 +29,11 @@ from . import _capi as C
 from .solver import Solver, comm_unique_id
 
 
-def plan(global_shape, nranks=1, rank=0, min_slab_planes=0):
+def plan(global_shape, nranks=1, rank=0, min_slab_planes=0, min_slab_voxels=0):
     """Per-level plan of one rank: list of dicts(size (x,y,z), z0, z1, distributed)."""
     d = C.default_desc()
     d.min_slab_planes = int(min_slab_planes)
+    d.min_slab_voxels = int(min_slab_voxels)
     dim = len(global_shape)
     d.dim = dim
     size = list(reversed(global_shape)) + [1] * (3 - dim)

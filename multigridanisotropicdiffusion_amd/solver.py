@@ -60,7 +60,8 @@ class Solver:
                  smoother=C.GAUSS_SEIDEL, iterations_per_grid=2, max_cycles=100,
                  number_of_steps=1, tolerance=1e-6, omega=2.0 / 3.0, verbose=False,
                  precision=C.PRECISION_AUTO, stall_guard=None, device=-1, tensor_kind=C.TENSOR_AUTO,
-                 nranks=1, rank=0, global_shape=None, gs_kernel=0, options=0, min_slab_planes=0):
+                 nranks=1, rank=0, global_shape=None, gs_kernel=0, options=0, min_slab_planes=0,
+                 min_slab_voxels=0):
         L = C.load()
         self.shape = tuple(int(s) for s in shape)  # this rank's slab
         gshape = tuple(global_shape) if global_shape is not None else self.shape
@@ -93,6 +94,7 @@ class Solver:
         d.gs_kernel = int(gs_kernel)
         d.options = int(options)
         d.min_slab_planes = int(min_slab_planes)
+        d.min_slab_voxels = int(min_slab_voxels)
         self._desc = d
         ctx = ctypes.c_void_p()
         C.check(L.mad_create(ctypes.byref(d), ctypes.byref(ctx)))

@@ -123,15 +123,23 @@ def test_plan_slabs_cover_and_align(nranks):
     assert plans[0][nl - 1]["dist"] == 0
 
 
-@pytest.mark.parametrize("nranks,msp,depths", [
-    (8, 0, [64, 32, 16, 8, 4]), (8, 16, [64, 32, 16]), (8, 64, [64]),
-    (4, 8, [128, 64, 32, 16, 8]), (2, 32, [256, 128, 64, 32]),
+@pytest.mark.parametrize("gshape,nranks,msp,msv,depths", [
+    # planes alone (min_slab_voxels 1)
+    ((512, 512, 512), 8, 0, 1, [64, 32, 16, 8, 4]), ((512, 512, 512), 8, 16, 1, [64, 32, 16]),
+    ((512, 512, 512), 8, 64, 1, [64]), ((512, 512, 512), 4, 8, 1, [128, 64, 32, 16, 8]),
+    ((512, 512, 512), 2, 32, 1, [256, 128, 64, 32]),
+    # the defaults: >= 4 planes and >= 128 K voxels per rank
+    ((512, 512, 512), 8, 0, 0, [64, 32, 16]), ((512, 512, 512), 4, 0, 0, [128, 64, 32]),
+    ((512, 512, 512), 2, 0, 0, [256, 128, 64, 32]), ((512, 1024, 1024), 8, 0, 0, [64, 32, 16, 8]),
+    # voxels alone
+    ((512, 512, 512), 8, 0, 1 << 20, [64, 32]),
 ])
-def test_plan_min_slab_planes(nranks, msp, depths):
-    """mad_desc.min_slab_planes: coarse levels stay distributed while every rank keeps that many
-    planes (level 0 always: >= 4); the rest is replicated (agglomeration)."""
+def test_plan_min_slab_planes(gshape, nranks, msp, msv, depths):
+    """mad_desc.min_slab_planes / min_slab_voxels: coarse levels stay distributed while every rank
+    keeps that many planes and voxels (level 0 always: >= 4 planes); the rest is replicated
+    (agglomeration)."""
     from multigridanisotropicdiffusion_amd import distributed as D
-    p = D.plan((512, 512, 512), nranks, nranks - 1, msp)
+    p = D.plan(gshape, nranks, nranks - 1, msp, msv)
     assert [q["z1"] - q["z0"] for q in p if q["distributed"]] == depths
     assert all(not q["distributed"] for q in p[len(depths):])
 

@@ -11,6 +11,9 @@ import synth
 pytestmark = pytest.mark.gpu
 
 SHAPE = (64, 48, 40)  # (z, y, x): levels (64,48,40) (32,24,20) (16,12,10)
+# keep coarse levels distributed down to 2 K voxels per rank on these small shapes (the default,
+# MAD_MIN_SLAB_VOXELS, replicates everything below level 0 here): the thin-slab paths under test
+DEEP = 2048
 
 
 def _single(fn, T, **kw):
@@ -28,7 +31,7 @@ def _multi(nranks, fn, T, **kw):
         s.set_tensor(T)
         s.setup()
         return fn(r, s)
-    return D.run_local(nranks, body, SHAPE, time_step=0.4, **kw)
+    return D.run_local(nranks, body, SHAPE, time_step=0.4, min_slab_voxels=DEEP, **kw)
 
 
 @pytest.mark.parametrize("nranks", [2, 4])
@@ -103,7 +106,7 @@ def test_slab_tensor_setup_is_bitwise(nranks):
     s = M.Solver(shape, time_step=0.4)
     ref = fn(None, s)
     s.close()
-    out = D.run_local(nranks, fn, shape, time_step=0.4)
+    out = D.run_local(nranks, fn, shape, time_step=0.4, min_slab_voxels=DEEP)
     for q in range(2):
         np.testing.assert_array_equal(np.concatenate([o[q] for o in out]), ref[q])
 
@@ -166,7 +169,8 @@ def test_single_launch_slab_sweeps_bitwise(nranks, gs_kernel, cycle):
         s.set_tensor(T)
         s.setup()
         return fn(r, s)
-    out = D.run_local(nranks, body, shape, time_step=0.4, gs_kernel=gs_kernel, cycle=cycle)
+    out = D.run_local(nranks, body, shape, time_step=0.4, gs_kernel=gs_kernel, cycle=cycle,
+                      min_slab_voxels=DEEP)
     np.testing.assert_array_equal(np.concatenate([o[0] for o in out]), ref[0])
     np.testing.assert_array_equal(np.concatenate([o[1] for o in out]), ref[1])
 
@@ -197,7 +201,7 @@ def test_solo_transport_times_one_rank():
     z0, z1 = D.slabs(shape, 4)[2]
     for cyc in (M.SMOOTHER, M.VCYCLE):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.1, cycle=cyc, nranks=4, rank=2,
-                     global_shape=shape)
+                     global_shape=shape, min_slab_voxels=DEEP)
         s.comm_init_solo()
         s.set_tensor(synth.random_spd(shape, seed=9))
         s.setup()
@@ -231,7 +235,7 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     base = M.capi.OPT_OVERLAP_RANK_SWEEP if overlap else 0
     for opt in (0, M.capi.OPT_EAGER_RANK_VCYCLE):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
-                     global_shape=shape, options=opt | base, gs_kernel=gs_kernel)
+                     global_shape=shape, min_slab_voxels=DEEP, options=opt | base, gs_kernel=gs_kernel)
         s.comm_init_solo()
         s.synth_tensor(kind=0, seed=9)
         s.setup()
@@ -266,7 +270,7 @@ def test_rccl_solo_equals_solo(cycle, gs_kernel):
     out = {}
     for mode in ("solo", "rccl"):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
-                     global_shape=shape, gs_kernel=gs_kernel)
+                     global_shape=shape, min_slab_voxels=DEEP, gs_kernel=gs_kernel)
         if mode == "solo":
             s.comm_init_solo()
         else:

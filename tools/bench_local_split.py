@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def solo(ns, msp=0, gsk=0, opts=0, rccl=False):
+def solo(ns, msp=0, gsk=0, opts=0, rccl=False, msv=0):
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     S, sweeps, vcyc = 512, 20, 10
@@ -32,11 +32,12 @@ def solo(ns, msp=0, gsk=0, opts=0, rccl=False):
     for n in ns:
         r = n // 2
         z0, z1 = D.slabs((S, S, S), n)[r]
-        out = {"ranks": n, "rank": r, "slab": [z1 - z0, S, S], "min_slab_planes": msp, "gs_kernel": gsk, "options": opts,
+        out = {"ranks": n, "rank": r, "slab": [z1 - z0, S, S], "min_slab_planes": msp, "min_slab_voxels": msv, "gs_kernel": gsk, "options": opts,
                "transport": "rccl-solo" if rccl else "solo",
-               "distributed_levels": sum(p["distributed"] for p in D.plan((S, S, S), n, r, msp))}
+               "distributed_levels": sum(p["distributed"] for p in D.plan((S, S, S), n, r, msp, msv))}
         for cyc, key in ((M.SMOOTHER, "sweep"), (M.VCYCLE, "vcycle")):
-            kw = dict(nranks=n, rank=r, global_shape=(S, S, S), min_slab_planes=msp) if n > 1 else {}
+            kw = dict(nranks=n, rank=r, global_shape=(S, S, S), min_slab_planes=msp,
+                      min_slab_voxels=msv) if n > 1 else {}
             s = M.Solver((z1 - z0, S, S), time_step=0.1, cycle=cyc, gs_kernel=gsk, options=opts, **kw)
             if n > 1:
                 if rccl:
@@ -83,11 +84,16 @@ def main():
         i = args.index("--options")
         opts = int(args[i + 1])
         del args[i:i + 2]
+    msv = 0
+    if "--msv" in args:  # mad_desc.min_slab_voxels
+        i = args.index("--msv")
+        msv = int(args[i + 1])
+        del args[i:i + 2]
     rccl = "--rccl" in args  # --solo through RCCL (mad_comm_init_rccl_solo)
     if rccl:
         args.remove("--rccl")
     if args and args[0] == "--solo":
-        return solo([int(v) for v in (args[1:] or ["1", "2", "4", "8"])], msp, gsk, opts, rccl)
+        return solo([int(v) for v in (args[1:] or ["1", "2", "4", "8"])], msp, gsk, opts, rccl, msv)
     S, sweeps, vcyc = 512, 20, 3
     for n in [int(v) for v in (args or ["1", "2", "4", "8"])]:
         bar = threading.Barrier(n)
