@@ -222,7 +222,8 @@ def main():
     units_per_launch = float(shape[0] * shape[1] * shape[2]) * a.steps / max(1, launches)
     achieved = BYTES_PER_VOXEL_SMOOTH * units_per_launch / (kern_ms * 1e-3) / 1e9
     tag = f"{a.smoother}_{S}"
-    traffic = load_traffic(tag, kname)
+    # (the profile is of the whole 512^3 volume on one GPU: not a rank slab's launch)
+    traffic = load_traffic(tag, kname) if world == 1 else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
             "traffic": traffic["bytes_per_launch"] if traffic else None,
