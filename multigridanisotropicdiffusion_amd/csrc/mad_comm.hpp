@@ -234,7 +234,6 @@ class Comm {
   }
 
   bool active() const { return mode_ != NONE && nranks_ > 1; }
-  bool self() const { return self_; }
   // RCCL peer of neighbour rank q (RCCL-SOLO: every peer is this process's only rank)
   int peer(int q) const { return self_ ? 0 : (q + nranks_) % nranks_; }
   Mode mode() const { return mode_; }
