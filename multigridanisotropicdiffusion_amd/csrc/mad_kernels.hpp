@@ -820,12 +820,16 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
 // in gs_fused3_k), reads each point's coefficient record with wide buffer loads one
 // step ahead, and writes r (and optionally fp64 |r|^2 partials per workgroup).
 // One barrier per plane.  Needs the GHOST x/b planes and coefficient padding planes
-// of LevelData (masked lanes read inside them).
-template <typename T, int KIND, int TX, int TY, bool BREC = false>
+// of LevelData (masked lanes read inside them).  be / xe (MAD_FP32_REFINE's defect
+// correction): also be = (TE) r and xe = 0 at every point, the fp32 hierarchy's next rhs and
+// zero initial guess (convert_k + fill_k of r folded into this pass).
+template <typename T, int KIND, int TX, int TY, bool BREC = false, typename TE = T>
 __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const T* __restrict__ b,
                                                     T* __restrict__ r, const T* __restrict__ cf,
                                                     Geo g, Rat<T> rat, int zc, int ntx,
-                                                    double* __restrict__ part) {
+                                                    double* __restrict__ part,
+                                                    TE* __restrict__ be = nullptr,
+                                                    TE* __restrict__ xe = nullptr) {
   constexpr int NT = TX * TY;
   constexpr int RX = TX + 2, RY = TY + 2, PL = RX * RY;
   constexpr int UPT = (PL + NT - 1) / NT;
@@ -932,6 +936,11 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
     load_pt(m + 1);
     if (ok) {
       if (r) buf_store<T>(rv, buf_rsrc(r + (int64_t)m * sz + pbase), pt_off);  // null: norm only
+      if (be) {
+        const int64_t p = (int64_t)m * sz + pbase + ty * sy + tx;
+        be[p] = (TE)rv;
+        xe[p] = TE(0);
+      }
       sq += (double)rv * (double)rv;
     }
   }

@@ -890,7 +890,10 @@ class Solver final : public SolverBase {
   double residual(int l, bool want_norm) override { return residual_impl(l, want_norm, true); }
 
   // fp64 residual of the refined level-0 system: r64 = b64 - A64 u64 (+ ||r||^2 partials),
-  // the reference operator in fp64 (coefficient records cf64_, g from the fp64 tensor)
+  // the reference operator in fp64 (coefficient records cf64_, g from the fp64 tensor).  3D
+  // levels of >= 16 x 16 write the fp32 hierarchy's next rhs b = (T) r and x = 0 in the same
+  // pass instead of r64 (refine_emitted_; else run_refine converts r64 and fills x)
+  bool refine_emitted_ = false;
   double residual64() {
     LevelData<T>& L = lv_[0];
     if (c_->comm.active() && c_->geom[0].distributed) {
@@ -911,9 +914,11 @@ class Solver final : public SolverBase {
       REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
       auto go = [&](auto K) {
         constexpr int KD = decltype(K)::value;
-        hipLaunchKernelGGL((resid3_k<double, KD, TX, TY>), dim3((unsigned)nparts), dim3(TX * TY), 0,
-                           c_->stream, u64_, b64_, r64_, cf64_, g, rat64_, zc, ntx, part_);
+        hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T>), dim3((unsigned)nparts), dim3(TX * TY),
+                           0, c_->stream, u64_, b64_, (double*)nullptr, cf64_, g, rat64_, zc, ntx, part_,
+                           L.b, L.x);
       };
+      refine_emitted_ = true;
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
       else go(std::integral_constant<int, KISO>{});
@@ -925,6 +930,7 @@ class Solver final : public SolverBase {
         hipLaunchKernelGGL((residual_k<double, D.value, K.value>), gr, BLK, 0, c_->stream, u64_, b64_,
                            r64_, cf64_, g, rat64_, part_);
       });
+      refine_emitted_ = false;
     }
     HIP_CHECK(hipGetLastError());
     return std::sqrt(finish_norm2(nparts, c_->geom[0].distributed));
@@ -1553,8 +1559,13 @@ class Solver final : public SolverBase {
       const unsigned window = (d.cycle == MAD_SMOOTHER) ? 50 : 5;
       bool stalled = false;
       do {  // MAD.hxx:207-246
-        to_fp32_rhs(r64_);
-        fill(0, MAD_X, 0.0);
+        if (refine_emitted_) {  // b = (T) r and x = 0 written by residual64's pass
+          L0.b_halo_ok = L0.brec_ok = false;
+          x_changed(0);
+        } else {
+          to_fp32_rhs(r64_);
+          fill(0, MAD_X, 0.0);
+        }
         if (d.cycle == MAD_SMOOTHER) {
           smooth(0, 1);
         } else {
