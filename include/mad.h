@@ -82,6 +82,9 @@ typedef enum mad_precision {
    profiles/r03_rank_serial_ab.md) */
 #define MAD_MIN_SLAB_PLANES 4
 #define MAD_MIN_SLAB_VOXELS 131072
+/* defaults of mad_desc.coarse_dense_max / coarse_block_unknowns (the DirectSolver, DS.hxx:32-147) */
+#define MAD_COARSE_DENSE_MAX 8192
+#define MAD_COARSE_BLOCK_UNKNOWNS 2048
 
 typedef enum mad_tensor_kind {
   MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */
@@ -134,7 +137,15 @@ typedef struct mad_desc {
   int32_t min_slab_voxels;       /* 0 = default (MAD_MIN_SLAB_VOXELS): below ~128 K voxels per rank a
                                     level's exchanges (one RCCL round trip per sweep) cost more than
                                     sweeping the whole level on every rank */
-  int32_t reserved[5];
+  int32_t coarse_dense_max;      /* DirectSolver (DS.hxx:32-147): a coarsest level of up to this many
+                                    unknowns is factored densely into an explicit inverse (one GEMV
+                                    per solve); a larger one (thin volumes, or any axis < 12: the
+                                    whole grid, GH.hxx:36-59) by the block-plane LU.  0 = default
+                                    (MAD_COARSE_DENSE_MAX) */
+  int32_t coarse_block_unknowns; /* block-plane LU: unknowns per diagonal block (max(1, this / plane
+                                    size) planes of the longest axis).  0 = default
+                                    (MAD_COARSE_BLOCK_UNKNOWNS) */
+  int32_t reserved[3];
 } mad_desc;
 
 /* mad_desc.options: MAD_OPT_EAGER_RANK_VCYCLE keeps a multi-rank V-cycle eager instead of

@@ -82,7 +82,9 @@ class MadDesc(ctypes.Structure):
         ("options", ctypes.c_uint32),
         ("min_slab_planes", ctypes.c_int32),
         ("min_slab_voxels", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 5),
+        ("coarse_dense_max", ctypes.c_int32),
+        ("coarse_block_unknowns", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 

@@ -1842,24 +1842,15 @@ __global__ void __launch_bounds__(256) build_coef3_k(const double* __restrict__ 
 //   g_x = 1/4 delta_x a_x + 1/2 delta_y e_xy + 1/2 delta_z e_xz   (and cyclically)
 // with delta the reference's 2h-scaled differences (central; one-sided second order at
 // the border, delta_f).  Every kernel evaluates g through these helpers on the same
-// T-typed inputs in the same order, so a g recomputed inside a sweep (gs_fusedg_k) is
-// bit-identical to the g build_g_k stores for the per-point kernels.
-// The border formulas are written as a central difference against a ghost value one point
-// outside the face, f(-1) = 3 f(0) - 3 f(1) + f(2) (and mirrored at the top): f(1) - f(-1) =
-// -3 f(0) + 4 f(1) - f(2), the reference's one-sided second-order difference, exactly in real
-// arithmetic.  The g-free sweep stores these ghosts beside the tensor (build_gt_k) and takes
-// plain central differences everywhere, so it rounds like this function at the faces too.
-template <typename T>
-__device__ __forceinline__ T gghost(T f0, T f1, T f2) {
-#pragma clang fp contract(off)
-  return (T(3) * f0 - T(3) * f1) + f2;
-}
-
+// T-typed inputs in the same order.
+// At the faces the reference's one-sided second-order differences, in its order
+// (GH.hxx:454-462): (-3 f(0) + 4 f(1)) - f(2) at the low face, (3 f(0) - 4 f(-1)) + f(-2)
+// at the high face (the fp64 refine build, build_coef*_k, evaluates the same expressions).
 template <typename T>
 __device__ __forceinline__ T gdelta(T fm2, T fm1, T f0, T fp1, T fp2, bool lo, bool hi) {
 #pragma clang fp contract(off)
-  if (lo) return fp1 - gghost(f0, fp1, fp2);
-  if (hi) return gghost(f0, fm1, fm2) - fm1;
+  if (lo) return (T(-3) * f0 + T(4) * fp1) - fp2;
+  if (hi) return (T(3) * f0 - T(4) * fm1) + fm2;
   return fp1 - fm1;
 }
 

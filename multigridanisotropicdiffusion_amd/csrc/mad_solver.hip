@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/mad.h"
+#include "mad_coarse.hpp"
 #include "mad_comm.hpp"
 #include "mad_kernels.hpp"
 
@@ -1118,8 +1119,11 @@ class Solver final : public SolverBase {
     LevelData<T>& L = lv_[l];
     const int n = (int)L.g.N;
     REQUIRE(!c_->geom[l].distributed, MAD_ERR_UNSUPPORTED, "coarsest level must be replicated");
-    hipLaunchKernelGGL((coarse_solve_k<T>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c_->stream,
-                       inv_, L.b, L.x, n);
+    if (cblk_.active())
+      cblk_.solve<T>(L.b, L.x, c_->stream);  // large coarsest level: block-plane LU (mad_coarse.hpp)
+    else
+      hipLaunchKernelGGL((coarse_solve_k<T>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c_->stream,
+                         inv_, L.b, L.x, n);
     HIP_CHECK(hipGetLastError());
   }
 
@@ -1448,8 +1452,9 @@ class Solver final : public SolverBase {
         ++it;
         trace(step, relres);
         hist.push_back(relres);
-        // fp32 floor guard: best relres not improved by 1% within `window` cycles
-        if (d.stall_guard && hist.size() > window && relres < 1e-3) {
+        // fp32 floor guard: best relres not improved by 1% within `window` cycles (only while the
+        // tolerance is unmet: a cycle that reaches it ends the step as converged)
+        if (d.stall_guard && hist.size() > window && relres < 1e-3 && relres > d.tolerance) {
           double prev_best = INFINITY;
           for (size_t q = 0; q + window < hist.size(); ++q) prev_best = std::min(prev_best, hist[q]);
           double recent = INFINITY;
@@ -1584,7 +1589,7 @@ class Solver final : public SolverBase {
         trace(step, relres);
         hist.push_back(relres);
         // fallback only: the fp64 residual keeps falling where plain fp32 stalls
-        if (d.stall_guard && hist.size() > window && relres < 1e-3) {
+        if (d.stall_guard && hist.size() > window && relres < 1e-3 && relres > d.tolerance) {
           double prev_best = INFINITY;
           for (size_t q = 0; q + window < hist.size(); ++q) prev_best = std::min(prev_best, hist[q]);
           double recent = INFINITY;
@@ -1736,6 +1741,7 @@ class Solver final : public SolverBase {
   double* scal_ = nullptr;
   double* hscal_ = nullptr;
   double* inv_ = nullptr;
+  CoarseBlocks cblk_;  // coarsest levels above DENSE_COARSE_MAX unknowns
   void* scratch_ = nullptr;
   size_t scratch_cap_ = 0;
   // replicated-level hand-over (multi-GPU)
@@ -1768,6 +1774,7 @@ class Solver final : public SolverBase {
     if (scal_) (void)hipFree(scal_);
     if (hscal_) (void)hipHostFree(hscal_);
     if (inv_) (void)hipFree(inv_);
+    cblk_.release();
     if (scratch_) (void)hipFree(scratch_);
     if (gathered_) (void)hipFree(gathered_);
     if (full_x_) (void)hipFree(full_x_);
@@ -1981,73 +1988,99 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipFree(cf64));
   }
 
-  // dense A of the coarsest level from its fp64 coefficient fields (mirror
-  // ghosts folded), DS.hxx:32-88 semantics
-  void build_coarse_inverse() {
+  // Row p of the coarsest operator from its fp64 coefficient records (mirror ghosts
+  // folded): emit(col, v) for A[p][col] += v, in the order the dense matrix was always
+  // assembled (DS.hxx:32-88 semantics; GH.hxx:298-516 via the matrix-free coefficients)
+  template <typename Emit>
+  void coarse_row(int64_t p, Emit&& emit) const {
     const int dim = c_->dim;
     const int kind = c_->kind;
     const LevelGeom& G = c_->geom[c_->nlev - 1];
-    const int64_t n = G.N;
-    REQUIRE(n <= 16384, MAD_ERR_UNSUPPORTED,
-            "coarsest grid has " + std::to_string(n) +
-                " unknowns (> 16384): an axis shorter than 12 leaves the whole grid to the "
-                "direct solver (GH.hxx:36-59)");
     const double* cf = coarse_coef64_.data();
     const int na = (kind == KISO) ? 1 : dim;
     const int nc = coef_count(dim, kind);
-    std::vector<double> A((size_t)n * n, 0.0);
     const int64_t nx = G.n[0], ny = G.n[1], nz = G.n[2];
+    const int64_t i = p % nx, j = (p / nx) % ny, k = p / (nx * ny);
     const double r1 = (G.h[0] * G.h[0]) / (G.h[1] * G.h[1]);
     const double r2 = (G.h[0] * G.h[0]) / (G.h[2] * G.h[2]);
-    for (int64_t k = 0; k < nz; ++k)
-      for (int64_t j = 0; j < ny; ++j)
-        for (int64_t i = 0; i < nx; ++i) {
-          const int64_t p = i + nx * (j + ny * k);
-          // point-interleaved, x-parity-split records (mad_kernels.hpp, cidx)
-          const double* rec =
-              cf + (nx * (j + ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * nc;
-          double a[3], g[3], e[3] = {0, 0, 0};
-          if (kind == KISO) {
-            a[0] = rec[0]; a[1] = rec[0] * r1; a[2] = rec[0] * r2;
-          } else {
-            for (int d = 0; d < dim; ++d) a[d] = rec[d];
-          }
-          for (int d = 0; d < dim; ++d) g[d] = rec[na + d];
-          if (kind == KFULL)
-            for (int q = 0; q < dim * (dim - 1) / 2; ++q) e[q] = rec[na + dim + q];
-          const int64_t xm = (i == 0) ? 1 : i - 1, xp = (i == nx - 1) ? nx - 2 : i + 1;
-          const int64_t ym = (j == 0) ? 1 : j - 1, yp = (j == ny - 1) ? ny - 2 : j + 1;
-          const int64_t zm = (k == 0) ? 1 : k - 1, zp = (k == nz - 1) ? nz - 2 : k + 1;
-          auto idx = [&](int64_t ii, int64_t jj, int64_t kk) { return ii + nx * (jj + ny * kk); };
-          double* row = &A[(size_t)p * n];
-          double D = 1.0 + 2.0 * (a[0] + a[1] + (dim == 3 ? a[2] : 0.0));
-          row[p] += D;
-          // A u = D u - S  =>  A[p][q] -= coefficient of u(q) in S
-          row[idx(xp, j, k)] -= a[0] + g[0];
-          row[idx(xm, j, k)] -= a[0] - g[0];
-          row[idx(i, yp, k)] -= a[1] + g[1];
-          row[idx(i, ym, k)] -= a[1] - g[1];
-          if (dim == 3) {
-            row[idx(i, j, zp)] -= a[2] + g[2];
-            row[idx(i, j, zm)] -= a[2] - g[2];
-          }
-          if (kind == KFULL) {
-            row[idx(xp, yp, k)] -= e[0];
-            row[idx(xp, ym, k)] += e[0];
-            row[idx(xm, yp, k)] += e[0];
-            row[idx(xm, ym, k)] -= e[0];
-            if (dim == 3) {
-              row[idx(xp, j, zp)] -= e[1];
-              row[idx(xp, j, zm)] += e[1];
-              row[idx(xm, j, zp)] += e[1];
-              row[idx(xm, j, zm)] -= e[1];
-              row[idx(i, yp, zp)] -= e[2];
-              row[idx(i, yp, zm)] += e[2];
-              row[idx(i, ym, zp)] += e[2];
-              row[idx(i, ym, zm)] -= e[2];
-            }
-          }
-        }
+    // point-interleaved, x-parity-split records (mad_kernels.hpp, cidx)
+    const double* rec = cf + (nx * (j + ny * k) + ((i & 1) ? (nx + 1) / 2 + (i >> 1) : (i >> 1))) * nc;
+    double a[3], g[3], e[3] = {0, 0, 0};
+    if (kind == KISO) {
+      a[0] = rec[0]; a[1] = rec[0] * r1; a[2] = rec[0] * r2;
+    } else {
+      for (int d = 0; d < dim; ++d) a[d] = rec[d];
+    }
+    for (int d = 0; d < dim; ++d) g[d] = rec[na + d];
+    if (kind == KFULL)
+      for (int qq = 0; qq < dim * (dim - 1) / 2; ++qq) e[qq] = rec[na + dim + qq];
+    const int64_t xm = (i == 0) ? 1 : i - 1, xp = (i == nx - 1) ? nx - 2 : i + 1;
+    const int64_t ym = (j == 0) ? 1 : j - 1, yp = (j == ny - 1) ? ny - 2 : j + 1;
+    const int64_t zm = (k == 0) ? 1 : k - 1, zp = (k == nz - 1) ? nz - 2 : k + 1;
+    auto idx = [&](int64_t ii, int64_t jj, int64_t kk) { return ii + nx * (jj + ny * kk); };
+    emit(p, 1.0 + 2.0 * (a[0] + a[1] + (dim == 3 ? a[2] : 0.0)));
+    // A u = D u - S  =>  A[p][q] -= coefficient of u(q) in S
+    emit(idx(xp, j, k), -(a[0] + g[0]));
+    emit(idx(xm, j, k), -(a[0] - g[0]));
+    emit(idx(i, yp, k), -(a[1] + g[1]));
+    emit(idx(i, ym, k), -(a[1] - g[1]));
+    if (dim == 3) {
+      emit(idx(i, j, zp), -(a[2] + g[2]));
+      emit(idx(i, j, zm), -(a[2] - g[2]));
+    }
+    if (kind == KFULL) {
+      emit(idx(xp, yp, k), -e[0]);
+      emit(idx(xp, ym, k), e[0]);
+      emit(idx(xm, yp, k), e[0]);
+      emit(idx(xm, ym, k), -e[0]);
+      if (dim == 3) {
+        emit(idx(xp, j, zp), -e[1]);
+        emit(idx(xp, j, zm), e[1]);
+        emit(idx(xm, j, zp), e[1]);
+        emit(idx(xm, j, zm), -e[1]);
+        emit(idx(i, yp, zp), -e[2]);
+        emit(idx(i, yp, zm), e[2]);
+        emit(idx(i, ym, zp), e[2]);
+        emit(idx(i, ym, zm), -e[2]);
+      }
+    }
+  }
+
+  // DirectSolver setup (DS.hxx:32-88: vnl_sparse_lu of the coarsest operator, any size).
+  // Up to mad_desc.coarse_dense_max unknowns: dense LU -> explicit inverse, one GEMV per
+  // solve.  Above: the block-plane LU of mad_coarse.hpp (thin volumes: 512x512x64 coarsens
+  // to 64x64x8; any axis < 12 leaves the whole grid to the direct solver, GH.hxx:36-59).
+  void build_coarse_inverse() {
+    const int dim = c_->dim;
+    const LevelGeom& G = c_->geom[c_->nlev - 1];
+    const int64_t n = G.N;
+    const int64_t dense_max = c_->d.coarse_dense_max > 0 ? c_->d.coarse_dense_max : MAD_COARSE_DENSE_MAX;
+    const int target = c_->d.coarse_block_unknowns > 0 ? c_->d.coarse_block_unknowns : MAD_COARSE_BLOCK_UNKNOWNS;
+    if (n > dense_max) {
+      const size_t need = CoarseBlocks::estimate_bytes(dim, G.n, target);
+      size_t free_b = 0, total_b = 0;
+      HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      REQUIRE(need < free_b / 10 * 9, MAD_ERR_UNSUPPORTED,
+              "coarsest grid has " + std::to_string(n) + " unknowns: its direct solver needs " +
+                  std::to_string(need >> 20) + " MiB of device memory, " + std::to_string(free_b >> 20) +
+                  " MiB free (an axis shorter than 12 leaves the whole grid to the direct solver, "
+                  "GH.hxx:36-59)");
+      bool ok = false;
+      try {
+        ok = cblk_.build(dim, G.n, target,
+                         [&](int64_t p, const CoarseBlocks::Emit& emit) { coarse_row(p, emit); },
+                         c_->stream);
+      } catch (const std::runtime_error& e) {
+        throw MadError(MAD_ERR_UNSUPPORTED, e.what());
+      }
+      REQUIRE(ok, MAD_ERR_SINGULAR, "coarsest operator is singular");
+      return;
+    }
+    std::vector<double> A((size_t)n * n, 0.0);
+    for (int64_t p = 0; p < n; ++p) {
+      double* row = &A[(size_t)p * n];
+      coarse_row(p, [&](int64_t col, double v) { row[col] += v; });
+    }
     HIP_CHECK(hipMalloc(&inv_, sizeof(double) * n * n));
     REQUIRE(invert_dense_device(n, A, inv_, c_->stream), MAD_ERR_SINGULAR,
             "coarsest operator is singular");
@@ -2310,6 +2343,9 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
     REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP)) == 0, MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
+    REQUIRE(d->coarse_dense_max >= 0 && d->coarse_dense_max <= 65536, MAD_ERR_INVALID,
+            "coarse_dense_max must be in [0, 65536]");
+    REQUIRE(d->coarse_block_unknowns >= 0, MAD_ERR_INVALID, "coarse_block_unknowns must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");
     c->d = *d;

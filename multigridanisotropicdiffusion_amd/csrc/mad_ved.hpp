@@ -358,6 +358,9 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
       cur += rb[r];
       const auto tp = tplanes(r);
       const int nzb = tp.second - tp.first;
+      // ved_block_k indexes a block with 32-bit offsets
+      REQUIRE(3 * (int64_t)nzb * ny * nxr < ((int64_t)1 << 31), MAD_ERR_UNSUPPORTED,
+              "VED transpose block exceeds 2^31 elements (use more ranks)");
       hipLaunchKernelGGL((ved_block_k<T, false>), dim3(flat_blocks(3 * (int64_t)nzb * ny * nxr)), dim3(256), 0, st,
                          Z3, (T*)sp[r], nx, ny, xa, nxr, tp.first, nzb, 3);
     }
@@ -367,6 +370,8 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     for (int q = 0; q < P_; ++q) {
       if (q == me) continue;
       const int qa = xr(q).first, qn = xr(q).second - xr(q).first;
+      REQUIRE(3 * (int64_t)nzm * ny * qn < ((int64_t)1 << 31), MAD_ERR_UNSUPPORTED,
+              "VED transpose block exceeds 2^31 elements (use more ranks)");
       hipLaunchKernelGGL((ved_block_k<T, true>), dim3(flat_blocks(3 * (int64_t)nzm * ny * qn)), dim3(256), 0, st, Z3,
                          (T*)rp[q], nx, ny, qa, qn, mp.first, nzm, 3);
     }

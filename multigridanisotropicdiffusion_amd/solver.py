@@ -61,7 +61,7 @@ class Solver:
                  number_of_steps=1, tolerance=1e-6, omega=2.0 / 3.0, verbose=False,
                  precision=C.PRECISION_AUTO, stall_guard=None, device=-1, tensor_kind=C.TENSOR_AUTO,
                  nranks=1, rank=0, global_shape=None, gs_kernel=0, options=0, min_slab_planes=0,
-                 min_slab_voxels=0):
+                 min_slab_voxels=0, coarse_dense_max=0, coarse_block_unknowns=0):
         L = C.load()
         self.shape = tuple(int(s) for s in shape)  # this rank's slab
         gshape = tuple(global_shape) if global_shape is not None else self.shape
@@ -95,6 +95,8 @@ class Solver:
         d.options = int(options)
         d.min_slab_planes = int(min_slab_planes)
         d.min_slab_voxels = int(min_slab_voxels)
+        d.coarse_dense_max = int(coarse_dense_max)
+        d.coarse_block_unknowns = int(coarse_block_unknowns)
         self._desc = d
         ctx = ctypes.c_void_p()
         C.check(L.mad_create(ctypes.byref(d), ctypes.byref(ctx)))
@@ -130,11 +132,23 @@ class Solver:
 
     def set_tensor_planes(self, tensor, first_plane):
         """SetDiffusionTensor from global planes [first_plane, ...) only (AoS (z, y, x, ncomp)
-        or SoA (ncomp, z, y, x) of those planes; mad_set_tensor_planes)."""
-        nc = self.dim * (self.dim + 1) // 2
+        or SoA (ncomp, z, y, x) of those planes; mad_set_tensor_planes).  The in-plane shape
+        must be the grid's; the plane count is the array's."""
+        if self.dim != 3:
+            raise ValueError("set_tensor_planes takes z planes of a 3D grid; use set_tensor in 2D")
+        nc = 6
+        plane = tuple(reversed([self._desc.size[q] for q in range(2)]))  # (y, x)
         t = np.asarray(tensor)
-        if t.shape[0] == nc and t.ndim == self.dim + 1 and t.shape[-1] != nc:
+        aos_ok = t.ndim == 4 and t.shape[1:3] == plane and t.shape[3] == nc
+        soa_ok = t.ndim == 4 and t.shape[0] == nc and t.shape[2:] == plane
+        if aos_ok and soa_ok:
+            raise ValueError(f"tensor planes of shape {t.shape} are ambiguous (AoS or SoA)")
+        if soa_ok:
             t = np.moveaxis(t, 0, -1)
+        elif not aos_ok:
+            raise ValueError(f"tensor planes of shape {t.shape} do not match the grid: expected "
+                             f"AoS (planes, {plane[0]}, {plane[1]}, {nc}) or SoA "
+                             f"({nc}, planes, {plane[0]}, {plane[1]})")
         t = np.ascontiguousarray(t, dtype=np.float64 if t.dtype == np.float64 else np.float32)
         self._check(self._L.mad_set_tensor_planes(self._ctx, t.ctypes.data_as(ctypes.c_void_p),
                                                   C.F64 if t.dtype == np.float64 else C.F32,

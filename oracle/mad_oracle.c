@@ -13,8 +13,10 @@
  * PARITY UNPINNED (no reference golden vectors exist; reference not buildable).
  *
  * Deliberate, documented differences (rounding-level only):
- *  - the direct solver is a dense partial-pivot LU instead of vnl_sparse_lu
- *    (DS:81-86,129) -- both are exact solvers, results agree to fp64 rounding;
+ *  - the direct solver is a partial-pivot LU instead of vnl_sparse_lu
+ *    (DS:81-86,129): dense up to ORA_DENSE_MAX unknowns, banded above it (the
+ *    unknowns renumbered with the shortest axis innermost, LAPACK gbtrf/gbtrs
+ *    restated) -- all are exact solvers, results agree to fp64 rounding;
  *  - Interpolation scatters interior coarse points first and then all border
  *    points in x-fastest order; ITK's ImageBoundaryFacesCalculator visits the
  *    border faces in a different order (IGO.hxx:93-167), which only permutes
@@ -44,11 +46,16 @@ struct ora_ctx {
   ora_level lev[MAXLEV];
   int noff;          /* active offsets: 19 (3D, corners removed GH:632-653) / 9 (2D) */
   int off[27][3];    /* in Neighborhood index order (itkStencilImage.hxx:51-67) */
-  /* coarsest-level dense LU (replaces vnl_sparse_lu, DS:32-88) */
+  /* coarsest-level LU (replaces vnl_sparse_lu, DS:32-88): dense (kl == -1) or banded */
   long nlu;
   double *lu;
   long *piv;
+  long kl, ku;  /* banded: sub/super-diagonals of A in the renumbered order */
+  long *perm;   /* banded: natural (x-fastest) index -> band index */
 };
+
+/* dense LU up to this many unknowns (the golden fixtures' sizes), banded above */
+#define ORA_DENSE_MAX 4096
 
 static inline int nbidx(int ox, int oy, int oz) { return (ox + 1) + 3 * (oy + 1) + 9 * (oz + 1); }
 
@@ -316,6 +323,99 @@ static void lu_solve(long n, const double *a, const long *piv, double *x) {
   for (long i = n - 1; i >= 0; --i) { double s = x[i]; for (long j = i + 1; j < n; ++j) s -= a[i * n + j] * x[j]; x[i] = s / a[i * n + i]; }
 }
 
+/* ---------------------------------------------------------------- banded LU */
+/* LAPACK dgbtf2 / dgbtrs restated (unblocked, partial pivoting) on column-major band
+ * storage: A(i, j) at ab[(kv + i - j) + j * ldab], kv = kl + ku, ldab = 2 kl + ku + 1 (the
+ * kl extra super-diagonals hold U's fill from row interchanges). */
+static int band_factor(long n, long kl, long ku, double *ab, long *piv) {
+  const long kv = kl + ku, ldab = 2 * kl + ku + 1;
+  long ju = 0;
+  for (long j = 0; j < n; ++j) {
+    double *cj = ab + j * ldab;
+    long km = kl < n - 1 - j ? kl : n - 1 - j;
+    long p = 0;
+    double best = fabs(cj[kv]);
+    for (long i = 1; i <= km; ++i)
+      if (fabs(cj[kv + i]) > best) { best = fabs(cj[kv + i]); p = i; }
+    piv[j] = j + p;
+    if (best == 0.) return -1;
+    long jn = j + ku + p < n - 1 ? j + ku + p : n - 1;
+    if (jn > ju) ju = jn;
+    if (p != 0)
+      for (long c = j; c <= ju; ++c) {
+        double *cc = ab + c * ldab + kv - c;
+        double t = cc[j]; cc[j] = cc[j + p]; cc[j + p] = t;
+      }
+    const double inv = 1. / cj[kv];
+    for (long i = 1; i <= km; ++i) cj[kv + i] *= inv;
+#pragma omp parallel for schedule(static) if ((ju - j) * km > 200000)
+    for (long c = j + 1; c <= ju; ++c) {
+      double *cc = ab + c * ldab + kv - c;  /* cc[r] = A(r, c) */
+      const double f = cc[j];
+      if (f != 0.)
+        for (long i = 1; i <= km; ++i) cc[j + i] -= cj[kv + i] * f;
+    }
+  }
+  return 0;
+}
+
+static void band_solve(long n, long kl, long ku, const double *ab, const long *piv, double *x) {
+  const long kv = kl + ku, ldab = 2 * kl + ku + 1;
+  for (long j = 0; j < n; ++j) { /* L y = P b */
+    long p = piv[j];
+    if (p != j) { double t = x[j]; x[j] = x[p]; x[p] = t; }
+    long lm = kl < n - 1 - j ? kl : n - 1 - j;
+    const double *cj = ab + j * ldab + kv;
+    for (long i = 1; i <= lm; ++i) x[j + i] -= cj[i] * x[j];
+  }
+  for (long j = n - 1; j >= 0; --j) { /* U x = y, U with kl + ku super-diagonals */
+    const double *cj = ab + j * ldab + kv - j;  /* cj[r] = U(r, j) */
+    x[j] /= cj[j];
+    long i0 = j - kv > 0 ? j - kv : 0;
+    for (long i = i0; i < j; ++i) x[i] -= cj[i] * x[j];
+  }
+}
+
+/* band numbering of the coarsest grid: axes ordered by length (shortest innermost, the
+ * longest outermost), so the bandwidth is about the product of the two shorter axes */
+static void band_order(int dim, const long n[3], long *perm, long *kl_out, long *ku_out,
+                       const double *A) {
+  int ax[3] = {0, 1, 2};
+  for (int a = 0; a < dim; ++a)
+    for (int b = a + 1; b < dim; ++b)
+      if (n[ax[b]] < n[ax[a]] || (n[ax[b]] == n[ax[a]] && ax[b] < ax[a])) {
+        int t = ax[a]; ax[a] = ax[b]; ax[b] = t;
+      }
+  long st[3] = {0, 0, 0}, s = 1;
+  for (int a = 0; a < dim; ++a) { st[ax[a]] = s; s *= n[ax[a]]; }
+  long idx[3], kl = 0, ku = 0;
+  for (idx[2] = 0; idx[2] < n[2]; ++idx[2])
+    for (idx[1] = 0; idx[1] < n[1]; ++idx[1])
+      for (idx[0] = 0; idx[0] < n[0]; ++idx[0]) {
+        long p = idx[0] + n[0] * (idx[1] + n[1] * idx[2]);
+        perm[p] = idx[0] * st[0] + idx[1] * st[1] + idx[2] * st[2];
+      }
+  for (idx[2] = 0; idx[2] < n[2]; ++idx[2])
+    for (idx[1] = 0; idx[1] < n[1]; ++idx[1])
+      for (idx[0] = 0; idx[0] < n[0]; ++idx[0]) {
+        long p = idx[0] + n[0] * (idx[1] + n[1] * idx[2]);
+        for (int i = 0; i < 27; ++i) {
+          if (A[27 * p + i] == 0.) continue;
+          int o[3] = {i % 3 - 1, (i / 3) % 3 - 1, i / 9 - 1};
+          long q[3] = {idx[0] + o[0], idx[1] + o[1], idx[2] + o[2]};
+          int inside = 1;
+          for (int d = 0; d < 3; ++d)
+            if (q[d] < 0 || q[d] >= n[d]) inside = 0;
+          if (!inside) continue;
+          long d = perm[q[0] + n[0] * (q[1] + n[1] * q[2])] - perm[p];
+          if (d > ku) ku = d;
+          if (-d > kl) kl = -d;
+        }
+      }
+  *kl_out = kl;
+  *ku_out = ku;
+}
+
 /* ---------------------------------------------------------------- hierarchy */
 ora_ctx *ora_create(int dim, const long n0[3], const double h0[3], const double *tensor,
                     double dt) {
@@ -369,8 +469,18 @@ ora_ctx *ora_create(int dim, const long n0[3], const double h0[3], const double 
   ora_level *C = &L[c->nlev - 1];
   long n = C->N;
   c->nlu = n;
-  c->lu = (double *)calloc((size_t)n * n, sizeof(double));
+  c->kl = -1;
   c->piv = (long *)malloc(sizeof(long) * n);
+  long ldab = 0;
+  if (n > ORA_DENSE_MAX) {
+    c->perm = (long *)malloc(sizeof(long) * n);
+    band_order(dim, C->n, c->perm, &c->kl, &c->ku, C->A);
+    ldab = 2 * c->kl + c->ku + 1;
+    c->lu = (double *)calloc((size_t)n * ldab, sizeof(double));
+  } else {
+    c->lu = (double *)calloc((size_t)n * n, sizeof(double));
+  }
+  if (!c->lu) { ora_destroy(c); return NULL; }
   long idx[3];
   for (idx[2] = 0; idx[2] < C->n[2]; ++idx[2])
     for (idx[1] = 0; idx[1] < C->n[1]; ++idx[1])
@@ -385,10 +495,16 @@ ora_ctx *ora_create(int dim, const long n0[3], const double h0[3], const double 
             if (q[d] < 0 || q[d] >= C->n[d]) inside = 0;
           if (!inside) continue;
           long col = q[0] + C->n[0] * (q[1] + C->n[1] * q[2]);
-          c->lu[row * n + col] = C->A[27 * row + i];
+          if (c->kl < 0) {
+            c->lu[row * n + col] = C->A[27 * row + i];
+          } else if (C->A[27 * row + i] != 0.) {
+            long r = c->perm[row], k = c->perm[col];
+            c->lu[(c->kl + c->ku + r - k) + k * ldab] = C->A[27 * row + i];
+          }
         }
       }
-  if (lu_factor(n, c->lu, c->piv) != 0) { ora_destroy(c); return NULL; }
+  int fail = (c->kl < 0) ? lu_factor(n, c->lu, c->piv) : band_factor(n, c->kl, c->ku, c->lu, c->piv);
+  if (fail != 0) { ora_destroy(c); return NULL; }
   return c;
 }
 
@@ -397,6 +513,7 @@ void ora_destroy(ora_ctx *c) {
   for (int l = 0; l < c->nlev; ++l) free(c->lev[l].A);
   free(c->lu);
   free(c->piv);
+  free(c->perm);
   free(c);
 }
 
@@ -560,8 +677,16 @@ void ora_interpolate(const ora_ctx *c, int level, const double *coarse, double *
 
 /* DirectSolver::Solve, DS:91-147 */
 void ora_direct_solve(const ora_ctx *c, const double *b, double *x) {
-  memcpy(x, b, sizeof(double) * c->nlu);
-  lu_solve(c->nlu, c->lu, c->piv, x);
+  if (c->kl < 0) {
+    memcpy(x, b, sizeof(double) * c->nlu);
+    lu_solve(c->nlu, c->lu, c->piv, x);
+    return;
+  }
+  double *t = (double *)malloc(sizeof(double) * c->nlu);
+  for (long p = 0; p < c->nlu; ++p) t[c->perm[p]] = b[p];
+  band_solve(c->nlu, c->kl, c->ku, c->lu, c->piv, t);
+  for (long p = 0; p < c->nlu; ++p) x[p] = t[c->perm[p]];
+  free(t);
 }
 
 /* L2Norm, MAD:496-515 */

@@ -78,6 +78,13 @@ def pytest_sessionstart(session):
     _MP["job"] = dict(procs=procs, logs=logs, outdir=outdir, world=world)
 
 
+def pytest_collection_modifyitems(session, config, items):
+    """The RCCL rank job started at session start runs on every GPU (device 0 included): its
+    test goes first, so it is joined before any timing-sensitive or memory-heavy GPU test
+    shares the devices with it."""
+    items.sort(key=lambda it: 0 if "test_gpu_multiproc.py" in it.nodeid else 1)
+
+
 def multiproc_job(config):
     return _MP.get("job")
 

@@ -201,3 +201,38 @@ def test_openmp_colour_sweep_equals_serial(oracle_mod, nthreads):
         o = oracle_mod.Oracle(shape, (1.0,) * len(shape), T, 0.3)
         b = synth.image(shape, seed=3)
         np.testing.assert_array_equal(o.gs_color(0, b, b, nc), o.gs_color_omp(0, b, b, nc, nthreads))
+
+
+def _assembled(o, l):
+    """Dense A of level l from the oracle's 27-point stencils (DS.hxx:32-88 assembly)."""
+    shape = o.shape_at(l)
+    n = list(reversed(shape)) + [1] * (3 - len(shape))
+    N = int(np.prod(shape))
+    S = o.stencil(l)
+    A = np.zeros((N, N))
+    for p in range(N):
+        i, j, k = p % n[0], (p // n[0]) % n[1], p // (n[0] * n[1])
+        for s in range(27):
+            if S[p, s] == 0.0:
+                continue
+            q = (i + s % 3 - 1, j + (s // 3) % 3 - 1, k + s // 9 - 1)
+            A[p, q[0] + n[0] * (q[1] + n[1] * q[2])] += S[p, s]
+    return A
+
+
+@pytest.mark.parametrize("shape,spacing", [
+    ((10, 22, 24), (1.0, 0.9, 1.2)),   # maxDepth 0, 5280 unknowns: the banded LU
+    ((26, 9, 21), (0.8, 1.0, 1.1)),    # short y axis innermost, x / z outer
+    ((10, 520), (1.0, 0.7)),           # 2D, 5200 unknowns
+])
+def test_banded_direct_solve_is_exact(O, shape, spacing):
+    """Above 4096 unknowns the oracle's DirectSolver (DS.hxx:32-147) is a banded partial-pivot
+    LU of the renumbered operator (shortest axis innermost, LAPACK gbtrf/gbtrs restated); it
+    solves A x = b to fp64 rounding like vnl_sparse_lu and numpy's dense LU."""
+    o = O.Oracle(shape, spacing, synth.random_spd(shape, seed=21), 2.0)
+    assert o.num_levels == 1 and int(np.prod(shape)) > 4096
+    b = np.random.default_rng(4).random(shape)
+    x = o.direct_solve(b)
+    assert np.abs(o.residual(0, x, b)).max() < 1e-12 * np.abs(b).max()
+    ref = np.linalg.solve(_assembled(o, 0), b.ravel()).reshape(shape)
+    assert np.abs(x - ref).max() < 1e-11 * np.abs(ref).max()
