@@ -43,7 +43,11 @@ def parse():
     p.add_argument("--gs-kernel", type=int, default=0,
                    help="0 auto (fused v3), 1 per-colour passes, 2 fused v2, 3 fused v3")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=4.0,
+                   help="length of the secondary 128^3 CPU sample")
+    p.add_argument("--cpu-size", type=int, default=0,
+                   help="volume of the CPU baseline (default: the benched size)")
+    p.add_argument("--no-precision-cycles", action="store_true")
     return p.parse_args()
 
 
@@ -59,65 +63,99 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(seconds):
-    """fp64 oracle (restated reference algorithm, lexicographic GS, 1 thread) on a
-    bounded 128^3 sample of the same VED-form workload."""
+def host_cores():
+    """CPUs this process may run on (its affinity mask) and the machine's CPU count."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return avail, os.cpu_count() or avail
+
+
+def cpu_baseline(seconds, size):
+    """fp64 oracle (the restated reference algorithm, oracle/) on the benched workload itself:
+    the size^3 VED-form system, a fixed count of lexicographic GS sweeps and one V-cycle on one
+    thread (the reference is single-threaded; BASELINE.md's C4 plan), the 4-colour GS on the
+    host cores beside it, and the earlier 128^3 sample as a secondary field.  Setup (the
+    GridsHierarchy + DCA stencils, ~30 GB at 512^3) is not timed: the metric is per sweep."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle
     import synth
-    shape = (128, 128, 128)
+    avail, total = host_cores()
+    nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, avail))
+    shape = (size, size, size)
+    nvox = float(np.prod(shape))
+    t0 = time.perf_counter()
     T = synth.ved_form(shape)
     o = oracle.Oracle(shape, (1.0, 1.0, 1.0), T, 0.1)
+    del T
     b = synth.image(shape, seed=3)
+    t_setup = time.perf_counter() - t0
+    n_sweeps = 2
+    t0 = time.perf_counter()
+    x = b
+    for _ in range(n_sweeps):
+        x = o.gs_lex(0, x, b)
+    el = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    x = o.vcycle(x, b, smoother=oracle.GS_LEX, iterations_per_grid=2)
+    el_v = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    y = b
+    for _ in range(n_sweeps):
+        y = o.gs_color_omp(0, y, b, 4, nt)
+    el_p = time.perf_counter() - t0
+    nlev = o.num_levels
+    del o, x, y, b
+    out = {"value": nvox * n_sweeps / el / 1e6, "unit": "Mvoxel-smooths/s", "cores": 1, "kind": "port",
+           "cpu_model": cpu_model(), "host_cpus_available": avail, "host_cpus_total": total,
+           "sample": f"{size}^3 VED-form full tensor (the benched system), {n_sweeps} lexicographic GS "
+                     f"sweeps, fp64, 1 thread, oracle/ (line-faithful restatement of the ITK reference), "
+                     f"{el:.1f} s (setup {t_setup:.0f} s untimed)"}
+    out["vcycle"] = {"value": 1.0 / el_v, "unit": "V-cycles/s", "cores": 1, "kind": "port",
+                     "sample": f"{size}^3 VED-form full tensor, 1 V-cycle (nu = 2, lexicographic GS, "
+                               f"{nlev} levels), fp64, 1 thread, oracle/, {el_v:.1f} s"}
+    out["parallel"] = {"value": nvox * n_sweeps / el_p / 1e6, "unit": "Mvoxel-smooths/s", "cores": nt,
+                       "kind": "port", "sample": f"{size}^3 VED-form full tensor, {n_sweeps} 4-colour GS "
+                       f"sweeps on {nt} OpenMP threads, fp64, oracle/, {el_p:.1f} s"}
+    # secondary: the bounded 128^3 sample of earlier rounds (same workload, smaller volume)
+    s128 = (128, 128, 128)
+    o = oracle.Oracle(s128, (1.0, 1.0, 1.0), synth.ved_form(s128), 0.1)
+    b = synth.image(s128, seed=3)
     x = b.copy()
     n = 0
     t0 = time.perf_counter()
     while True:
         x = o.gs_lex(0, x, b)
         n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    nvox = float(np.prod(shape))
-    out = {"value": nvox * n / el / 1e6, "unit": "Mvoxel-smooths/s", "cores": 1, "kind": "port",
-           "cpu_model": cpu_model(),
-           "sample": f"128^3 VED-form full tensor, {n} lexicographic GS sweeps, fp64, "
-                     f"oracle/ (line-faithful restatement of the ITK reference), {el:.1f} s"}
-    # beside it: the same restatement's multicolour GS (the GPU's sweep order) on the host
-    # cores this job may use (OpenMP; the box exports OMP_NUM_THREADS = its CPU share)
-    nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1))
-    x = b.copy()
-    m = 0
-    t0 = time.perf_counter()
-    while True:
-        x = o.gs_color_omp(0, x, b, 4, nt)
-        m += 1
         el2 = time.perf_counter() - t0
-        if el2 >= seconds / 2:
+        if el2 >= seconds:
             break
-    out["parallel"] = {"value": nvox * m / el2 / 1e6, "unit": "Mvoxel-smooths/s", "cores": nt,
-                       "kind": "port", "sample": f"128^3 VED-form full tensor, {m} 4-colour GS "
-                       f"sweeps on {nt} OpenMP threads, fp64, oracle/, {el2:.1f} s"}
-    # the V-cycle line (BASELINE.md's C4 plan: fixed sweeps and V-cycles): whole V-cycles of
-    # the restated reference (MAD.hxx:341-493, nu = 2, lexicographic GS, 1 thread) on the
-    # 128^3 sample; the 512^3 figure scales it by the voxel count (the work is linear in N)
-    x = b.copy()
-    k = 0
-    t0 = time.perf_counter()
-    while True:
-        x = o.vcycle(x, b, smoother=oracle.GS_LEX, iterations_per_grid=2)
-        k += 1
-        el3 = time.perf_counter() - t0
-        if el3 >= seconds / 2:
-            break
-    out["vcycle"] = {"value": k / el3, "unit": "V-cycles/s (128^3 sample)", "cores": 1, "kind": "port",
-                     "value_512_equiv": k / el3 / 64.0,
-                     "sample": f"128^3 VED-form full tensor, {k} V-cycles (nu = 2, lexicographic GS, "
-                               f"{o.num_levels} levels), fp64, oracle/, {el3:.1f} s; value_512_equiv = "
-                               f"value / 64 (voxel count)"}
+    out["sample_128"] = {"value": float(np.prod(s128)) * n / el2 / 1e6, "unit": "Mvoxel-smooths/s",
+                         "cores": 1, "kind": "port",
+                         "sample": f"128^3 VED-form full tensor, {n} lexicographic GS sweeps, fp64, {el2:.1f} s"}
     return out
+
+
+def run_cycle_ms(M, shape, prec, cycles, **kw):
+    """Milliseconds per solver cycle inside mad_run (the reference's loop: cycle, fp64 residual,
+    host convergence check; MAD.hxx:207-246) at Tolerance 1e-30, so every run takes `cycles`
+    cycles: median difference of mad_get_cycle_trace's timestamps, cycles 2 .. K of the second
+    run (the first captures the V-cycle graph)."""
+    import numpy as np
+    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, precision=prec, cycle=M.VCYCLE,
+                 tolerance=1e-30, max_cycles=cycles, stall_guard=0, **kw)
+    s.synth_tensor(kind=0, seed=4)
+    s.setup()
+    img = np.full(shape, 50.0, dtype=np.float32)
+    img[::3] = 100.0
+    s.run(img)
+    s.run(img)
+    t = [q[2] for q in s.cycle_trace()]
+    s.close()
+    return float(np.median(np.diff(t)[1:]) * 1e3)
 
 
 def load_traffic(tag, kernel_sig):
@@ -263,8 +301,22 @@ def main():
         "device_ms_per_step": round(dev_ms / a.steps, 4),
         "roofline": roof,
     }
+    if world == 1 and not a.no_precision_cycles:
+        # the cycle mad_run runs at the reference tests' Tolerance 1e-10 (MAD_PRECISION_AUTO ->
+        # FP32_REFINE: fp32 V-cycle + fp64 residual / update), and in MAD_FP64 (the reference's
+        # arithmetic throughout), beside the plain fp32 cycle of the same loop
+        pc = {}
+        for key, prec in (("fp32", M.FP32), ("refine", M.FP32_REFINE), ("fp64", M.FP64)):
+            pc[key] = run_cycle_ms(M, gshape, prec, 8, smoother=sm, gs_kernel=a.gs_kernel)
+        line["run_ms_per_cycle"] = {k: round(v, 3) for k, v in pc.items()}
+        line["refine_vcycles_per_s"] = round(1e3 / pc["refine"], 2)
+        line["fp64_vcycles_per_s"] = round(1e3 / pc["fp64"], 2)
+        line["run_cycle_config"] = ("mad_run loop at Tolerance 1e-30 (8 cycles, median of cycles 2..8): "
+                                    "V-cycle + fp64 (refine / fp64) or fp32 residual norm + host check; "
+                                    "refine = MAD_FP32_REFINE, what MAD_PRECISION_AUTO resolves to at "
+                                    "the reference tests' 1e-10")
     if world == 1 and not a.no_cpu_baseline:
-        cb = cpu_baseline(a.cpu_seconds)
+        cb = cpu_baseline(a.cpu_seconds, a.cpu_size or S)
         line["cpu_baseline"] = cb
     else:
         line["cpu_baseline"] = None

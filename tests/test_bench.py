@@ -13,11 +13,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_cpu_baseline_leg_reports_the_oracle():
     sys.path.insert(0, ROOT)
     import bench
-    cb = bench.cpu_baseline(0.05)
+    cb = bench.cpu_baseline(0.05, 24)
     assert cb["value"] > 0 and cb["unit"] == "Mvoxel-smooths/s"
-    assert cb["cores"] == 1 and cb["kind"] == "port" and "128^3" in cb["sample"]
+    assert cb["cores"] == 1 and cb["kind"] == "port" and cb["sample"].startswith("24^3")
+    assert cb["host_cpus_available"] >= 1 and cb["host_cpus_total"] >= cb["host_cpus_available"]
     par = cb["parallel"]
     assert par["value"] > 0 and par["cores"] >= 1 and par["kind"] == "port"
+    assert cb["vcycle"]["value"] > 0 and cb["vcycle"]["unit"] == "V-cycles/s"
+    assert cb["sample_128"]["value"] > 0 and "128^3" in cb["sample_128"]["sample"]
 
 
 @pytest.mark.gpu
@@ -36,6 +39,8 @@ def test_bench_json_line(extra):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 4 and d["dtype"] == "f32"
     assert d["value"] > 0 and d["vcycles_per_s"] > 0
+    assert d["refine_vcycles_per_s"] > 0 and d["fp64_vcycles_per_s"] > 0
+    assert set(d["run_ms_per_cycle"]) == {"fp32", "refine", "fp64"}
     # value = voxels x steps / wall time
     assert abs(d["value"] - 256 ** 3 * 4 / (d["ms_per_step"] * 4e-3) / 1e6) <= 0.01 * d["value"]
     r = d["roofline"]

@@ -27,7 +27,7 @@ CASES = [
     ((9, 40, 30), 0),       # q = 270 (x, z inside y), 7 planes per block, last block 5 planes
     ((9, 40, 30), 1),       # one plane per block: 2 x 39 chained q x q products
     ((10, 1500), 0),        # 2D: planes of 10, 204 per block
-    ((11, 26, 50), 3000),   # q = 286, 10 planes per block, 5 blocks
+    ((10, 26, 50), 3000),   # q = 260 (x outermost), 11 planes per block, 5 blocks
 ]
 
 
