@@ -23,8 +23,9 @@
 //                                                then the other rows at once
 //     x_i = y_i - Dinv_i[:, last] (F_i x_{i+1}[first])   chain over the first planes,
 //                                                then the other rows at once
-//   so the sequential part is 2 (nb - 1) q x q products and everything else is
-//   bandwidth-parallel.  All arithmetic fp64 (the reference's), deterministic
+//   so the sequential part is 2 (nb - 1) q x q products -- with the chain's matrices
+//   KL_i = Dinv_i[last, first] E_i and KU_i = Dinv_i[first, last] F_i formed at setup,
+//   one GEMV launch per step -- and everything else is bandwidth-parallel.  All arithmetic fp64 (the reference's), deterministic
 //   (one wave per row, fixed reduction order): every rank that replicates the
 //   coarsest level computes the same bits.
 #pragma once
@@ -81,12 +82,28 @@ __global__ void __launch_bounds__(256) cs_dinv_k(const double* __restrict__ dinv
   if (lane == 0) cv[r] = s;
 }
 
-// Coupling update of block i = iblk0 + blockIdx.y:
+// One chain step: cv[row0 + r] -= K[r, :] . cv[src0 .. src0 + q), r < q (K = KL_i or KU_i,
+// q x q row-major); one wave per row.
+__global__ void __launch_bounds__(256) cs_chain_k(const double* __restrict__ K, double* __restrict__ cv, int q,
+                                                  int row0, int src0) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= q) return;
+  const double* a = K + (size_t)r * q;
+  const double* v = cv + src0;
+  double s = 0.0;
+#pragma unroll 4
+  for (int k = lane; k < q; k += 64) s += a[k] * v[k];
+  s = cs_wave_sum(s);
+  if (lane == 0) cv[row0 + r] -= s;
+}
+
+// The other rows of every coupled block i = iblk0 + blockIdx.y, after its chain:
 //   LOWER (UPPER = false): t = E_i cv[last plane of block i-1],  cv[rows] -= Dinv_i[rows, 0:q] t
 //   UPPER:                 t = F_i cv[first plane of block i+1], cv[rows] -= Dinv_i[rows, m-q:m] t
-// rows: CHAIN the coupling plane (LOWER: last plane, UPPER: first plane of block i),
-// otherwise the block's other rows.  t lives in LDS (q doubles); 8 rows per workgroup.
-template <bool UPPER, bool CHAIN>
+// rows: LOWER all but the block's last plane, UPPER all but its first.  t lives in LDS (q
+// doubles), formed once per workgroup of 32 rows (8 per wave).
+template <bool UPPER>
 __global__ void __launch_bounds__(256) cs_couple_k(const double* __restrict__ dinv, const int* __restrict__ ecol,
                                                    const double* __restrict__ eval, int ew,
                                                    double* __restrict__ cv, int n, int mb, int q, int iblk0) {
@@ -94,6 +111,8 @@ __global__ void __launch_bounds__(256) cs_couple_k(const double* __restrict__ di
   const int i = iblk0 + (int)blockIdx.y;
   const int r0 = i * mb;
   const int m = min(mb, n - r0);
+  const int nsel = m - q;
+  if ((int)blockIdx.x * 32 >= nsel) return;  // whole workgroup: past the block's rows
   const int src = UPPER ? r0 + m : r0 - q;
   const int* ec = ecol + (size_t)i * q * ew;
   const double* ev = eval + (size_t)i * q * ew;
@@ -103,17 +122,16 @@ __global__ void __launch_bounds__(256) cs_couple_k(const double* __restrict__ di
     t[k] = s;
   }
   __syncthreads();
-  const int nsel = CHAIN ? q : m - q;
-  const int base = CHAIN ? (UPPER ? 0 : m - q) : (UPPER ? q : 0);
+  const int base = UPPER ? q : 0;
   const int col0 = UPPER ? m - q : 0;
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int rr = (int)blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + h;
+  for (int h = 0; h < 8; ++h) {
+    const int rr = (int)blockIdx.x * 32 + (threadIdx.x >> 6) * 8 + h;
     if (rr >= nsel) break;
     const int lr = base + rr;
     const double* a = dinv + (size_t)i * mb * mb + (size_t)lr * m + col0;
     double s = 0.0;
+#pragma unroll 4
     for (int k = lane; k < q; k += 64) s += a[k] * t[k];
     s = cs_wave_sum(s);
     if (lane == 0) cv[r0 + lr] -= s;
@@ -138,6 +156,8 @@ struct CoarseBlocks {
   double* eval = nullptr;
   int* fcol = nullptr;   // F_i ELL (block nb - 1 unused)
   double* fval = nullptr;
+  double* kl = nullptr;  // chain matrices KL_i (q x q per block; block 0 unused)
+  double* ku = nullptr;  // KU_i (block nb - 1 unused)
   double* bp = nullptr;
   double* cv = nullptr;
   size_t device_bytes = 0;
@@ -146,11 +166,11 @@ struct CoarseBlocks {
 
   void release() {
     for (void* p : {(void*)dinv, (void*)perm, (void*)iperm, (void*)ecol, (void*)eval, (void*)fcol,
-                    (void*)fval, (void*)bp, (void*)cv})
+                    (void*)fval, (void*)kl, (void*)ku, (void*)bp, (void*)cv})
       if (p) (void)hipFree(p);
     dinv = nullptr;
     perm = iperm = ecol = fcol = nullptr;
-    eval = fval = bp = cv = nullptr;
+    eval = fval = kl = ku = bp = cv = nullptr;
     n = q = mb = nb = ew = 0;
     device_bytes = 0;
   }
@@ -171,7 +191,7 @@ struct CoarseBlocks {
     const int64_t P = planes_per_block((int)q, (int)no, target);
     const int64_t mb = P * q, nb = (no + P - 1) / P;
     const int64_t last = N - (nb - 1) * mb;
-    return (size_t)(((nb - 1) * mb * mb + last * last) * 8 + 3 * q * q * 8 + N * 160);
+    return (size_t)(((nb - 1) * mb * mb + last * last) * 8 + (2 * nb + 3) * q * q * 8 + N * 160);
   }
 
   using Emit = std::function<void(int64_t col, double val)>;
@@ -274,6 +294,8 @@ struct CoarseBlocks {
     dmalloc((void**)&eval, sizeof(double) * ne);
     dmalloc((void**)&fcol, sizeof(int) * ne);
     dmalloc((void**)&fval, sizeof(double) * ne);
+    dmalloc((void**)&kl, sizeof(double) * nb * q * q);
+    dmalloc((void**)&ku, sizeof(double) * nb * q * q);
     dmalloc((void**)&bp, sizeof(double) * N);
     dmalloc((void**)&cv, sizeof(double) * N);
     auto h2d = [&](void* d, const void* h, size_t bytes) {
@@ -350,6 +372,13 @@ struct CoarseBlocks {
         if (rocsolver_dgetrf(h, m, m, Di, m, ipiv, info + 2 * i) != rocblas_status_success ||
             rocsolver_dgetri(h, m, Di, m, ipiv, info + 2 * i + 1) != rocblas_status_success)
           throw std::runtime_error("rocsolver getrf/getri failed");
+        // chain matrices: KL_i = Dinv_i[last, first] E_i, KU_i = Dinv_i[first, last] F_i
+        if (i > 0)  // dE still holds E_i (the Schur update above)
+          rm_gemm(q, q, q, 1.0, Di + (size_t)(m - q) * m, m, dE, q, 0.0, kl + (size_t)i * q * q, q);
+        if (i < nb - 1) {
+          ell_dense(fcol + (size_t)i * q * ew, fval + (size_t)i * q * ew, ew, q, dF, q, (size_t)q * q);
+          rm_gemm(q, q, q, 1.0, Di + (m - q), m, dF, q, 0.0, ku + (size_t)i * q * q, q);
+        }
       }
       if (hipGetLastError() != hipSuccess) throw std::runtime_error("direct solver: launch failed");
       std::vector<int> hinfo(2 * nb);
@@ -377,19 +406,22 @@ struct CoarseBlocks {
     hipLaunchKernelGGL((cs_gather_k<T>), dim3(g1), b256, 0, stream, b, iperm, bp, n);
     hipLaunchKernelGGL(cs_dinv_k, dim3((unsigned)((n + 3) / 4)), b256, 0, stream, dinv, bp, cv, n, mb);
     const size_t lds = sizeof(double) * q;
-    const unsigned gc = (unsigned)((q + 7) / 8);
-    for (int i = 1; i < nb; ++i)
-      hipLaunchKernelGGL((cs_couple_k<false, true>), dim3(gc, 1), b256, lds, stream, dinv, ecol, eval, ew, cv, n,
-                         mb, q, i);
+    const unsigned gc = (unsigned)((q + 3) / 4);
+    const unsigned gr = (unsigned)((mb - q + 31) / 32);
+    for (int i = 1; i < nb; ++i) {  // y_i[last] = c_i[last] - KL_i y_{i-1}[last]
+      const int r0 = i * mb, m = std::min(mb, n - r0);
+      hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, kl + (size_t)i * q * q, cv, q, r0 + m - q,
+                         r0 - q);
+    }
     if (mb > q && nb > 1)
-      hipLaunchKernelGGL((cs_couple_k<false, false>), dim3((unsigned)((mb - q + 7) / 8), (unsigned)(nb - 1)), b256,
-                         lds, stream, dinv, ecol, eval, ew, cv, n, mb, q, 1);
-    for (int i = nb - 2; i >= 0; --i)
-      hipLaunchKernelGGL((cs_couple_k<true, true>), dim3(gc, 1), b256, lds, stream, dinv, fcol, fval, ew, cv, n,
-                         mb, q, i);
+      hipLaunchKernelGGL((cs_couple_k<false>), dim3(gr, (unsigned)(nb - 1)), b256, lds, stream, dinv, ecol, eval,
+                         ew, cv, n, mb, q, 1);
+    for (int i = nb - 2; i >= 0; --i)  // x_i[first] = y_i[first] - KU_i x_{i+1}[first]
+      hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, ku + (size_t)i * q * q, cv, q, i * mb,
+                         (i + 1) * mb);
     if (mb > q && nb > 1)
-      hipLaunchKernelGGL((cs_couple_k<true, false>), dim3((unsigned)((mb - q + 7) / 8), (unsigned)(nb - 1)), b256,
-                         lds, stream, dinv, fcol, fval, ew, cv, n, mb, q, 0);
+      hipLaunchKernelGGL((cs_couple_k<true>), dim3(gr, (unsigned)(nb - 1)), b256, lds, stream, dinv, fcol, fval,
+                         ew, cv, n, mb, q, 0);
     hipLaunchKernelGGL((cs_scatter_k<T>), dim3(g1), b256, 0, stream, cv, perm, x, n);
   }
 };
