@@ -52,7 +52,24 @@ struct ora_ctx {
   long *piv;
   long kl, ku;  /* banded: sub/super-diagonals of A in the renumbered order */
   long *perm;   /* banded: natural (x-fastest) index -> band index */
+  /* verbose trace (ora_take_trace) */
+  long ntr, captr;
+  int *tr_level, *tr_it;
+  double *tr_rel;
 };
+
+static void trace_push(ora_ctx *c, int level, int it, double rel) {
+  if (c->ntr == c->captr) {
+    c->captr = c->captr ? 2 * c->captr : 64;
+    c->tr_level = (int *)realloc(c->tr_level, sizeof(int) * c->captr);
+    c->tr_it = (int *)realloc(c->tr_it, sizeof(int) * c->captr);
+    c->tr_rel = (double *)realloc(c->tr_rel, sizeof(double) * c->captr);
+  }
+  c->tr_level[c->ntr] = level;
+  c->tr_it[c->ntr] = it;
+  c->tr_rel[c->ntr] = rel;
+  ++c->ntr;
+}
 
 /* dense LU up to this many unknowns (the golden fixtures' sizes), banded above */
 #define ORA_DENSE_MAX 4096
@@ -514,6 +531,9 @@ void ora_destroy(ora_ctx *c) {
   free(c->lu);
   free(c->piv);
   free(c->perm);
+  free(c->tr_level);
+  free(c->tr_it);
+  free(c->tr_rel);
   free(c);
 }
 
@@ -712,17 +732,28 @@ static void smooth(const ora_ctx *c, const ora_params *p, int level, const doubl
 static void vcycle_rec(ora_ctx *c, const ora_params *p, int level, const double *x,
                        const double *b, double *out) {
   ora_level *L = &c->lev[level];
+  long N = L->N;
+  /* verbose only: rhsNorm (MAD:352) and the relative residual of the current iterate */
+  double *vr = p->verbose ? (double *)malloc(sizeof(double) * N) : NULL;
+  double rhsNorm = p->verbose ? ora_l2norm(N, b) : 0.;
+#define VERBOSE_LINE(it_, sol_)                                   \
+  if (p->verbose) {                                               \
+    ora_residual(c, level, (sol_), b, vr);                        \
+    trace_push(c, level, (it_), ora_l2norm(N, vr) / rhsNorm);     \
+  }
   if (level == c->nlev - 1) { /* MAD:356-371 */
     ora_direct_solve(c, b, out);
+    VERBOSE_LINE(-1, out);
+    free(vr);
     return;
   }
-  long N = L->N;
   double *cur = (double *)malloc(sizeof(double) * N);
   double *tmp = (double *)malloc(sizeof(double) * N);
   memcpy(cur, x, sizeof(double) * N); /* ImageDuplicator, MAD:375-379 */
   for (unsigned n = 0; n < p->iterations_per_grid; ++n) { /* MAD:384-411 */
     smooth(c, p, level, cur, b, tmp);
     double *t = cur; cur = tmp; tmp = t;
+    VERBOSE_LINE((int)n + 1, cur);
   }
   ora_residual(c, level, cur, b, tmp); /* MAD:389 */
   ora_level *Cl = &c->lev[level + 1];
@@ -733,12 +764,26 @@ static void vcycle_rec(ora_ctx *c, const ora_params *p, int level, const double 
   vcycle_rec(c, p, level + 1, xc, bc, oc); /* MAD:418-420 */
   ora_interpolate(c, level, oc, tmp);      /* MAD:422 */
   for (long i = 0; i < N; ++i) cur[i] += tmp[i]; /* MAD:424-435 */
+  VERBOSE_LINE(0, cur); /* MAD:437-448 */
   for (unsigned n = 0; n < p->iterations_per_grid; ++n) { /* MAD:460-487 */
     smooth(c, p, level, cur, b, tmp);
     double *t = cur; cur = tmp; tmp = t;
+    VERBOSE_LINE((int)n + 1, cur);
   }
+#undef VERBOSE_LINE
   memcpy(out, cur, sizeof(double) * N);
-  free(cur); free(tmp); free(bc); free(xc); free(oc);
+  free(cur); free(tmp); free(bc); free(xc); free(oc); free(vr);
+}
+
+long ora_take_trace(ora_ctx *c, long cap, int *level, int *it, double *relres) {
+  long n = c->ntr;
+  for (long i = 0; i < n && i < cap; ++i) {
+    if (level) level[i] = c->tr_level[i];
+    if (it) it[i] = c->tr_it[i];
+    if (relres) relres[i] = c->tr_rel[i];
+  }
+  c->ntr = 0;
+  return n;
 }
 
 /* FullMultiGrid, MAD:300-338 */

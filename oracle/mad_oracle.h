@@ -76,6 +76,11 @@ int ora_run(ora_ctx *c, const ora_params *p, const double *input, double *output
 
 /* single V-cycle / FMG on level 0 (for per-cycle parity checks) */
 void ora_vcycle(ora_ctx *c, const ora_params *p, const double *x, const double *b, double *out);
+/* Verbose trace of the V-cycles run since the last call (params.verbose != 0): the per-level
+ * relative residuals the reference prints (MAD.hxx:356-371, 384-411, 437-487), in print order:
+ * level, it (-1 direct solver, 0 "initial" after the correction, n >= 1 after sweep n), relres.
+ * Copies min(cap, count) entries, returns count, and clears the trace. */
+long ora_take_trace(ora_ctx *c, long cap, int *level, int *it, double *relres);
 void ora_fmg(ora_ctx *c, const ora_params *p, const double *b, double *out);
 
 #ifdef __cplusplus

@@ -78,6 +78,8 @@ def lib():
         L.ora_run.restype = ctypes.c_int
         L.ora_vcycle.argtypes = [ctypes.c_void_p, ctypes.POINTER(OraParams), dp, dp, dp]
         L.ora_fmg.argtypes = [ctypes.c_void_p, ctypes.POINTER(OraParams), dp, dp]
+        L.ora_take_trace.argtypes = [ctypes.c_void_p, ctypes.c_long, ip, ip, dp]
+        L.ora_take_trace.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -204,6 +206,18 @@ class Oracle:
         out = self._out(0)
         lib().ora_vcycle(self._c, ctypes.byref(p), _dp(self._in(x)), _dp(self._in(b)), _dp(out))
         return out
+
+    def vcycle_verbose(self, x, b, **kw):
+        """One V-cycle with the verbose trace; returns (output, [(level, it, relres), ...])."""
+        L = lib()
+        L.ora_take_trace(self._c, 0, None, None, None)
+        out = self.vcycle(x, b, verbose=1, **kw)
+        cap = 1 << 16
+        lv = (ctypes.c_int * cap)()
+        it = (ctypes.c_int * cap)()
+        rr = (ctypes.c_double * cap)()
+        n = L.ora_take_trace(self._c, cap, lv, it, rr)
+        return out, [(lv[i], it[i], rr[i]) for i in range(min(n, cap))]
 
     def fmg(self, b, **kw):
         p = params(**kw)

@@ -269,6 +269,28 @@ def sort_by_magnitude(w):
     return e
 
 
+def scale_responses(img, spacing, scales, alpha, beta, gamma, kind="recursive"):
+    """Vesselness of every scale (UpdateVesselness's candidates, VED.hxx:215-299), stacked:
+    (len(scales), *img.shape).  Used to find scale near-ties (the strict argmax, VED.hxx:272)."""
+    out = []
+    for sigma in scales:
+        H = hessian(img, spacing, sigma, kind)
+        A = np.empty(img.shape + (3, 3))
+        A[..., 0, 0], A[..., 0, 1], A[..., 0, 2] = H[..., 0], H[..., 1], H[..., 2]
+        A[..., 1, 0], A[..., 1, 1], A[..., 1, 2] = H[..., 1], H[..., 3], H[..., 4]
+        A[..., 2, 0], A[..., 2, 1], A[..., 2, 2] = H[..., 2], H[..., 4], H[..., 5]
+        w = np.linalg.eigh(A)[0]
+        out.append(vesselness(sort_by_magnitude(w), alpha, beta, gamma))
+    return np.stack(out)
+
+
+def near_ties(img, spacing, scales, alpha, beta, gamma, rel=1e-6):
+    """Voxels whose two largest scale responses are within `rel` of each other (positive
+    response): where an fp32 Hessian may pick either scale's direction."""
+    ves = np.sort(scale_responses(img, spacing, scales, alpha, beta, gamma), axis=0)
+    return (ves[-1] > 0) & ((ves[-1] - ves[-2]) <= rel * ves[-1])
+
+
 def multiscale(img, spacing, scales, alpha, beta, gamma, kind="recursive"):
     """UpdateVesselness over all scales: (response, eigenvector columns Q)."""
     resp = None

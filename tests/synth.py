@@ -110,16 +110,24 @@ def image(shape, seed=1):
 
 def tube_phantom(S, seed=4):
     """C4's VED input: bright axis-aligned tubes (radius 2..6 voxels, intensity
-    200 on 0) plus N(0, 10^2) noise, fp32 (z, y, x) -- the volume tools/bench_ved.py times."""
+    200 on 0) plus N(0, 10^2) noise, fp32 (z, y, x) -- the volume tools/bench_ved.py times.
+    S: the cube's edge, or a (z, y, x) shape (C5: (512, 1024, 1024))."""
+    shape = (S, S, S) if np.isscalar(S) else tuple(int(n) for n in S)
+    cube = len(set(shape)) == 1
     rng = np.random.default_rng(seed)
-    img = rng.normal(0.0, 10.0, size=(S, S, S)).astype(np.float32)
-    g = np.arange(S, dtype=np.float32)
+    img = rng.normal(0.0, 10.0, size=shape).astype(np.float32)
     for axis in range(3):
-        prof = np.zeros((S, S), np.float32)
+        n1, n2 = [shape[a] for a in range(3) if a != axis]  # the tube's cross-section axes
+        g1 = np.arange(n1, dtype=np.float32)
+        g2 = np.arange(n2, dtype=np.float32)
+        prof = np.zeros((n1, n2), np.float32)
         for _ in range(64 // 3 + (1 if axis < 64 % 3 else 0)):
-            a, b = rng.uniform(8, S - 8, size=2)
+            if cube:
+                a, b = rng.uniform(8, n1 - 8, size=2)
+            else:
+                a, b = rng.uniform(8, n1 - 8), rng.uniform(8, n2 - 8)
             r = rng.uniform(2, 6)
-            prof += 200.0 * np.exp(-((g[:, None] - a) ** 2 + (g[None, :] - b) ** 2) / (2 * r * r))
+            prof += 200.0 * np.exp(-((g1[:, None] - a) ** 2 + (g2[None, :] - b) ** 2) / (2 * r * r))
         if axis == 0:
             img += prof[None, :, :]
         elif axis == 1:

@@ -128,7 +128,7 @@ def test_ved_filter_full_volume_fp64(M, oracle_mod, volume, ved_ref):
 
 
 @pytest.mark.timeout(400)
-def test_ved_filter_full_volume_fp32(M, oracle_mod, volume):
+def test_ved_filter_full_volume_fp32(M, oracle_mod, volume, ved_ref):
     """fp32 storage: the tensor matches the oracle's within 1e-3 except at scale near-ties (the
     strict argmax over scales, VED.hxx:272, that an fp32 Hessian cannot resolve), and the
     diffusion -- the hot path, solved to the reference's 1e-10 by the default precision
@@ -144,8 +144,24 @@ def test_ved_filter_full_volume_fp32(M, oracle_mod, volume):
     T, _ = v.tensor(img)
     Tr, _ = VO.ved_tensor(x, sp, p["scales"], p["alpha"], p["beta"], p["gamma"], p["epsilon"],
                           p["omega"], p["sensitivity"])
+    # every tensor mismatch above 1e-3 must sit on a scale near-tie (both directions valid)
+    tie = VO.near_ties(x, sp, p["scales"], p["alpha"], p["beta"], p["gamma"])
     bad = np.abs(T - Tr).max(axis=0) > 1e-3
-    assert bad.mean() < 1e-4, np.argwhere(bad)[:5]
+    assert not (bad & ~tie).any(), np.argwhere(bad & ~tie)[:5]
+    assert tie.mean() < 1e-3
     ref32, _ = _oracle_solve(oracle_mod, x, sp, T)
     assert relmax(out, ref32) < 1e-5
+    # and against the oracle's whole pipeline (its own fp64 tensor): within 1e-5 away from the
+    # near-tie voxels' neighbourhoods (a tie voxel's other valid direction moves the solution
+    # locally), everywhere within the bound the tie voxels allow
+    ref, _ = ved_ref
+    near = tie.copy()
+    for ax in range(3):
+        for sh in (-3, -2, -1, 1, 2, 3):
+            near |= np.roll(tie, sh, axis=ax)
+    err = np.abs(out - ref) / np.abs(ref).max()
+    print(f"fp32 VED vs oracle pipeline: max {err.max():.2e}, off ties {err[~near].max():.2e}, "
+          f"ties {int(tie.sum())}")
+    assert err[~near].max() < 1e-5
+    assert err.max() < 1e-3
     v.close()

@@ -66,3 +66,42 @@ def test_c4_pipeline_run(phantom):
     dx_in = np.std(np.diff(phantom[::8], axis=2))
     dx_out = np.std(np.diff(out[::8], axis=2))
     assert dx_out < 0.9 * dx_in, (dx_out, dx_in)
+
+
+@pytest.mark.timeout(600)
+def test_c4_ved_on_8_rank_slabs_matches_single(phantom):
+    """The partitioned VED at C4 size: 8 in-process ranks (threads on one device, the LOCAL
+    transport) -- recursive Hessian z / y passes on each rank's x range, the 8-way transpose of
+    the three z-pass volumes (Comm::exchange_blocks), x pass + vesselness on the rank's tensor
+    planes, z-slab diffusion -- against the one-GPU pipeline, bit for bit."""
+    import threading
+    import zlib
+    import multigridanisotropicdiffusion_amd as M
+    kw = dict(epsilon=EPS, omega=OMEGA, sensitivity=SENS, diffusion_iterations=2, tolerance=TOL,
+              precision=M.FP32)
+    v = M.VED(phantom.shape, **kw)
+    ref, rst = v.run(phantom, out_dtype=np.float32)
+    v.close()
+    nranks = 8
+    outs, errs = [None] * nranks, []
+    key = zlib.crc32(repr(("ved_c4", phantom.shape, nranks)).encode())
+
+    def worker(r):
+        try:
+            w = M.VED(phantom.shape, nranks=nranks, rank=r, **kw)
+            w.comm_init_local(key)
+            outs[r] = w.run(phantom, out_dtype=np.float32)
+            w.close()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append((r, e))
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    full = np.concatenate([o[0] for o in outs])
+    assert full.shape == phantom.shape
+    assert all(o[1]["total_cycles"] == rst["total_cycles"] for o in outs)
+    np.testing.assert_array_equal(full, ref)
