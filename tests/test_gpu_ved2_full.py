@@ -144,8 +144,11 @@ def test_ved_filter_full_volume_fp32(M, oracle_mod, volume, ved_ref):
     T, _ = v.tensor(img)
     Tr, _ = VO.ved_tensor(x, sp, p["scales"], p["alpha"], p["beta"], p["gamma"], p["epsilon"],
                           p["omega"], p["sensitivity"])
-    # every tensor mismatch above 1e-3 must sit on a scale near-tie (both directions valid)
-    tie = VO.near_ties(x, sp, p["scales"], p["alpha"], p["beta"], p["gamma"])
+    # every tensor mismatch above 1e-3 must sit on a scale near-tie (both directions valid):
+    # the oracle's two best scales within 1e-5 relative, the accuracy of the fp32 vesselness
+    # (exp terms of fp32 eigenvalues; measured here: voxel (94, 88, 118), scales 0.775 / 1.245
+    # at 0.48292448 / 0.48292526, 1.6e-6 apart, the fp32 mode keeps 0.775, tools/debug_ved2_voxel.py)
+    tie = VO.near_ties(x, sp, p["scales"], p["alpha"], p["beta"], p["gamma"], rel=1e-5)
     bad = np.abs(T - Tr).max(axis=0) > 1e-3
     assert not (bad & ~tie).any(), np.argwhere(bad & ~tie)[:5]
     assert tie.mean() < 1e-3
