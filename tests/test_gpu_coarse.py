@@ -123,3 +123,60 @@ def test_depth0_volume_run_matches_oracle(oracle_mod):
         assert st["num_levels"] == 1 and st["last_relres"] <= 1e-10, st
         assert relmax(out, ref) < tol, (prec, relmax(out, ref))
         s.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_thin_volume_rank_slabs_match_single(nranks):
+    """Rank slabs (in-process transport) of a thin volume whose replicated coarsest level takes the
+    block-plane LU (32 x 256 x 256 -> 8 x 64 x 64): every rank factors and solves it alike, so two
+    V-cycles equal the one-GPU run bit for bit."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (32, 256, 256)
+    T = synth.ved_form(shape)
+    x = synth.image(shape, seed=1)
+    b = synth.image(shape, seed=2)
+    s = M.Solver(shape, time_step=0.5, precision=M.FP32)
+    s.set_tensor(T)
+    s.setup()
+    assert s.shape_at(s.num_levels - 1) == (8, 64, 64)
+    s.upload(0, M.capi.X, x)
+    s.upload(0, M.capi.B, b)
+    s.vcycle()
+    s.vcycle()
+    ref = s.download(0, M.capi.X)
+    s.close()
+    sl = D.slabs(shape, nranks)
+
+    def body(r, s):
+        z0, z1 = sl[r]
+        s.set_tensor(T)
+        s.setup()
+        s.upload(0, M.capi.X, x[z0:z1])
+        s.upload(0, M.capi.B, b[z0:z1])
+        s.vcycle()
+        s.vcycle()
+        return s.download(0, M.capi.X)
+    outs = D.run_local(nranks, body, shape, time_step=0.5, precision=M.FP32)
+    np.testing.assert_array_equal(np.concatenate(outs), ref)
+
+
+@pytest.mark.timeout(600)
+def test_thin_volume_fmg_matches_oracle(oracle_mod):
+    """FullMultiGrid (MAD.hxx:300-338) on a volume with a large coarsest level: the coarsest
+    'V-cycles' of FMG are repeated direct solves, here the block-plane LU; fp64
+    against the oracle's FMG (banded LU) in the same colour order."""
+    import multigridanisotropicdiffusion_amd as M
+    shape = (40, 256, 256)
+    T = synth.ved_form(shape)
+    b = synth.image(shape, seed=3)
+    s = M.Solver(shape, time_step=0.5, precision=M.FP64)
+    s.set_tensor(T)
+    s.setup()
+    s.upload(0, M.capi.B, b)
+    s.fmg()
+    got = s.download(0, M.capi.X)
+    s.close()
+    o = oracle_mod.Oracle(shape, (1.0, 1.0, 1.0), T, 0.5)
+    ref = o.fmg(b, smoother=oracle_mod.GS_COLOR, ncolors=4, iterations_per_grid=2)
+    assert relmax(got, ref) < 1e-10
