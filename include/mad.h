@@ -159,6 +159,13 @@ typedef struct mad_desc {
    launch and, in a captured V-cycle graph, a second stream that slows every node's launch
    (DESIGN.md "Multi-GPU"). */
 #define MAD_OPT_OVERLAP_RANK_SWEEP 2u
+/* MAD_OPT_PEER_HALO: on rank slabs, a level's fused GS sweep stores its GHOST edge planes straight into
+   the neighbours' mailboxes (device memory mapped across processes: hipIpc handles exchanged over the
+   communicator) and counts its tiles in their counters while the rest of the sweep runs; the next
+   consumer of the ghost planes waits for the neighbours' counters and copies the mailbox in (one small
+   launch) -- no exchange after the sweep.  Levels whose sweeps are not fused single launches keep the
+   exchange.  Identical results.  Setup-time option (mad_setup maps the windows, collectively). */
+#define MAD_OPT_PEER_HALO 4u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

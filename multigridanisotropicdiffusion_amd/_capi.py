@@ -32,6 +32,7 @@ X, B, R = 0, 1, 2
 # mad_desc.options / mad_ved_desc.options
 OPT_EAGER_RANK_VCYCLE = 1
 OPT_OVERLAP_RANK_SWEEP = 2
+OPT_PEER_HALO = 4
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (

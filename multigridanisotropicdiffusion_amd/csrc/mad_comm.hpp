@@ -460,6 +460,59 @@ class Comm {
     }
   }
 
+  // Peer windows (MAD_OPT_PEER_HALO).  Every rank exposes one device allocation `base`; the
+  // neighbours' windows mapped into this process come back as lo (rank - 1) / hi (rank + 1), null
+  // where there is no neighbour.  RCCL: IPC handles all-gathered over the communicator and opened
+  // here (*ipc = true: close them with close_window); LOCAL: the pointers themselves; SOLO and
+  // RCCL-SOLO: the rank's own window stands in for both neighbours.  Collective.
+  void share_window(void* base, hipStream_t s, void** lo, void** hi, bool* ipc) {
+    *lo = *hi = nullptr;
+    *ipc = false;
+    if (mode_ == SOLO || (mode_ == RCCL && self_)) {
+      *lo = *hi = base;
+      return;
+    }
+    if (mode_ == LOCAL) {
+      HIPC_CHECK(hipStreamSynchronize(s));
+      group_->ptr[rank_] = base;
+      group_->barrier();
+      if (rank_ > 0) *lo = const_cast<void*>(group_->ptr[rank_ - 1]);
+      if (rank_ < nranks_ - 1) *hi = const_cast<void*>(group_->ptr[rank_ + 1]);
+      group_->barrier();
+      return;
+    }
+    if (mode_ != RCCL) return;
+    hipIpcMemHandle_t mine;
+    HIPC_CHECK(hipIpcGetMemHandle(&mine, base));
+    const size_t hb = sizeof(hipIpcMemHandle_t);
+    std::vector<char> all(hb * nranks_);
+    char* d = nullptr;
+    HIPC_CHECK(hipMalloc(&d, hb * (nranks_ + 1)));
+    HIPC_CHECK(hipMemcpyAsync(d + hb * nranks_, &mine, hb, hipMemcpyHostToDevice, s));
+    NCCL_CHECK(ncclAllGather(d + hb * nranks_, d, hb, ncclChar, comm_, s));
+    HIPC_CHECK(hipMemcpyAsync(all.data(), d, hb * nranks_, hipMemcpyDeviceToHost, s));
+    HIPC_CHECK(hipStreamSynchronize(s));
+    HIPC_CHECK(hipFree(d));
+    auto open = [&](int r, void** p) {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, all.data() + hb * r, hb);
+      HIPC_CHECK(hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess));
+    };
+    if (rank_ > 0) open(rank_ - 1, lo);
+    if (rank_ < nranks_ - 1) open(rank_ + 1, hi);
+    *ipc = true;
+  }
+  static void close_window(void* p, bool ipc) {
+    if (p && ipc) (void)hipIpcCloseMemHandle(p);
+  }
+
+  // host barrier of the in-process transport (no-op for the others)
+  void local_barrier(hipStream_t s) {
+    if (mode_ != LOCAL) return;
+    HIPC_CHECK(hipStreamSynchronize(s));
+    group_->barrier();
+  }
+
   // every rank holds nz_global / nranks planes; gather all slabs in rank order
   void allgather_slabs(const void* slab, void* full, int64_t plane, int64_t nz_global, size_t esz,
                        hipStream_t s) {

@@ -420,12 +420,28 @@ struct FusedGeom {
 // communication stream, waiting on those counters, exchanges the halo while the rest
 // of the sweep runs -- one launch per sweep instead of boundary + interior launches.
 
-template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false>
+//
+// Peer halo (PEER, MAD_OPT_PEER_HALO): the edge chunks also store their first GHOST output
+// planes into the neighbour's mailbox (po.dst[0] bottom edge -> rank - 1, po.dst[1] top edge ->
+// rank + 1, addressed with the chunk's own plane stride, so the reflected top chunk fills the
+// mailbox downward) and, once a tile's GHOST planes are out, count the tile in the neighbour's
+// counter (po.sig[0] / po.sig[1]) with a system-scope release; the neighbour's stream waits on
+// that counter and copies the mailbox into its ghost planes (Solver::peer_resolve).
+
+// where a PEER sweep's edge planes go (null: no neighbour on that side)
+template <typename T>
+struct PeerOut {
+  T* dst[2];
+  uint32_t* sig[2];
+};
+
+template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false,
+          bool PEER = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
                                                         int zbase, int zstride, int flip_last,
-                                                        uint32_t* __restrict__ sig) {
+                                                        uint32_t* __restrict__ sig, PeerOut<T> po) {
   constexpr int NC = (KIND == KFULL) ? 4 : 2;
   using FG = FusedGeom<NC, TX, TY>;
   constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
@@ -491,7 +507,9 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   const int ulo = zlo_g ? -(GHOST - 1) : 0;
   const int uhi = zhi_g ? g.nz + GHOST - 1 : g.nz;
   // an edge chunk of a rank slab signals once its first GHOST planes are final
-  const bool signals = sig != nullptr && z0 == 0 && zlo_g;
+  T* const pdst = PEER ? po.dst[flip ? 1 : 0] : nullptr;
+  uint32_t* const psig = PEER ? po.sig[flip ? 1 : 0] : (sig ? sig + (flip ? 1 : 0) : nullptr);
+  const bool signals = (PEER ? pdst != nullptr : sig != nullptr) && z0 == 0 && zlo_g;
   // first step with its plane parity normalised to even (global z), last step
   const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + zpar) & 1);
   const int kend = z1 + NC - 2;
@@ -736,15 +754,75 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
           for (int e = 0; e < OPT; ++e)
             if (oglb[e] >= 0)
               buf_store<T>(*reinterpret_cast<const T*>(P + olds[e]), ro, (uint32_t)oglb[e]);
+          if constexpr (PEER) {
+            if (signals && mo < GHOST) {  // an edge plane: also into the neighbour's mailbox
+              const __amdgpu_buffer_rsrc_t rp = buf_rsrc(pdst + (int64_t)mo * sz);
+#pragma unroll
+              for (int e = 0; e < OPT; ++e)
+                if (oglb[e] >= 0)
+                  buf_store<T>(*reinterpret_cast<const T*>(P + olds[e]), rp, (uint32_t)oglb[e]);
+            }
+          }
           if (signals && mo == GHOST - 1) {
             // the edge planes 0..GHOST-1 of this tile are stored: release them, count in
-            __threadfence();
+            if (PEER)
+              __threadfence_system();
+            else
+              __threadfence();
             __syncthreads();
-            if (tid == 0)
-              __hip_atomic_fetch_add(sig + (flip ? 1 : 0), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tid == 0) __hip_atomic_fetch_add(psig, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
       }
+    }
+  }
+}
+
+// Peer halo, consumer side: wait for the neighbours' edge planes, copy the two mailboxes into
+// the ghost planes.  blockIdx.y = side (0: from rank - 1 into the lower ghost planes, 1: from
+// rank + 1 into the upper ones; a null destination = no neighbour there).  ctl is this rank's
+// control block: counters [buffer * 2 + side] the neighbours' sweeps count their tiles into
+// (ci = buffer * 2), a ticket, an error word.  Thread 0 of every block polls its side's counter
+// until all `tiles` edge tiles are in (system-scope acquire of uncached memory, so the stores of
+// the other GPU are visible), giving up after `tmo` wall-clock ticks with the error word set (a
+// peer that died must not hang this GPU); the last block to finish resets the counters, which no
+// neighbour touches again before this rank's next sweep has signalled it (Solver::peer_resolve).
+// The mailboxes are uncached, so the copy reads what the neighbour stored; the ghost planes are
+// then ordinary stream-ordered data for the kernels that follow.
+__global__ void __launch_bounds__(256) peer_unpack_k(char* __restrict__ dlo, const char* __restrict__ slo,
+                                                     char* __restrict__ dhi, const char* __restrict__ shi,
+                                                     uint64_t bytes, uint32_t* __restrict__ ctl, int ci,
+                                                     uint32_t tiles, uint64_t tmo) {
+  const int side = blockIdx.y;
+  char* d = side ? dhi : dlo;
+  const char* src = side ? shi : slo;
+  if (d) {
+    if (threadIdx.x == 0) {
+      uint32_t* cnt = ctl + ci + side;
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < tiles) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > tmo) {
+          __hip_atomic_store(ctl + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((uintptr_t)d | (uintptr_t)src | bytes) & 15) == 0) {
+      for (uint64_t i = t0; i < bytes / 16; i += stride) ((uint4*)d)[i] = ((const uint4*)src)[i];
+    } else {
+      for (uint64_t i = t0; i < bytes / 4; i += stride) ((uint32_t*)d)[i] = ((const uint32_t*)src)[i];
+    }
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t nb = gridDim.x * gridDim.y;
+    if (__hip_atomic_fetch_add(ctl + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) {
+      if (dlo) __hip_atomic_store(ctl + ci, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (dhi) __hip_atomic_store(ctl + ci + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(ctl + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -296,6 +296,19 @@ struct LevelData {
   // (signal memory, [0] bottom / [1] top) and the sweeps issued so far
   uint32_t* sig = nullptr;
   uint32_t sig_epoch = 0;
+  // peer halo (MAD_OPT_PEER_HALO, Solver::setup_peer): the fused sweep stores its edge planes
+  // straight into the neighbours' mailboxes.  phys: the ping-pong pair's x / t at setup (buffer
+  // identity: mailbox and counter index); win: this rank's window (uncached: mailboxes
+  // [buffer * 2 + side] of GHOST planes, then the control block: counters [buffer * 2 + side],
+  // ticket, error word); win_lo / win_hi: the neighbours' windows mapped here
+  T* phys[2] = {nullptr, nullptr};
+  char* win = nullptr;
+  char* win_lo = nullptr;
+  char* win_hi = nullptr;
+  bool win_ipc = false;
+  bool peer = false;
+  bool x_peer_pending = false;  // x's ghost planes arrive by peer stores: resolve before use
+  uint32_t peer_tiles = 0;
 };
 // z-depth of a rank slab's boundary chunks (>= GHOST; 4 measured 0.231 vs 0.228 ms per 8-rank
 // sweep, profiles/r02_slab_tiles.log)
@@ -345,6 +358,8 @@ class Solver final : public SolverBase {
       L.b = L.alloc[1] + margin + L.ghost;
       L.r = L.alloc[2] + margin + L.ghost;
       L.t = L.alloc[3] + margin + L.ghost;
+      L.phys[0] = L.x;
+      L.phys[1] = L.t;
       // coefficient records, point-interleaved (mad_kernels.hpp, cidx); 3D levels keep
       // GHOST coefficient planes per side: neighbour planes on rank slabs (the fused
       // sweep recomputes colours on them), padding for masked border lanes otherwise
@@ -417,7 +432,102 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipHostMalloc(&hscal_, sizeof(double) * 4, hipHostMallocDefault));
     build_operators();
     build_coarse_inverse();
+    setup_peer();
     HIP_CHECK(hipStreamSynchronize(c->stream));
+  }
+
+  // ------------------------------------------------------------- peer halo
+  // MAD_OPT_PEER_HALO: on every distributed level whose sweeps are fused single launches with
+  // both edge chunks reflected outward (>= 2 z-chunks of >= GHOST planes), the sweep itself stores
+  // its GHOST edge planes into the neighbours' mailboxes and counts its tiles in their counters;
+  // no exchange follows the sweep.  The next consumer of x's ghost planes waits for the
+  // neighbours' counters and copies the mailboxes in (peer_resolve, one small launch).  Collective
+  // (share_window); every rank takes the same decision (same plane counts on distributed levels).
+  static constexpr size_t PEER_CTL = 256;
+  size_t window_bytes(const LevelData<T>& L) const { return 4 * (size_t)L.ghost * sizeof(T) + PEER_CTL; }
+  T* mailbox(char* w, const LevelData<T>& L, int buf, int side) const {
+    return (T*)(w + (size_t)(buf * 2 + side) * (size_t)L.ghost * sizeof(T));
+  }
+  uint32_t* peer_ctl(char* w, const LevelData<T>& L) const {
+    return (uint32_t*)(w + 4 * (size_t)L.ghost * sizeof(T));
+  }
+  bool peer_eligible(int l) {
+    LevelData<T>& L = lv_[l];
+    if (!(c_->d.options & MAD_OPT_PEER_HALO) || !c_->comm.active() || !c_->geom[l].distributed) return false;
+    if (!use_fused(l) || c_->dim != 3) return false;
+    int tiles = 0, nchunks = 0;
+    fused_shape(L, &tiles, &nchunks);
+    const ZRange zr = whole_range(L.g.nz, tiles, fused_cfg());
+    return nchunks >= 2 && zr.zc >= GHOST;
+  }
+  void setup_peer() {
+    int wall_khz = 0;
+    if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, c_->device) != hipSuccess ||
+        wall_khz <= 0)
+      wall_khz = 100000;
+    peer_timeout_ticks_ = (uint64_t)wall_khz * 1000ull * 20ull;  // 20 s
+    for (size_t l = 0; l < lv_.size(); ++l) {
+      LevelData<T>& L = lv_[l];
+      if (!peer_eligible((int)l)) continue;
+      const size_t wb = window_bytes(L);
+      HIP_CHECK(hipExtMallocWithFlags((void**)&L.win, wb, hipDeviceMallocUncached));
+      HIP_CHECK(hipMemsetAsync(L.win, 0, wb, c_->stream));
+      void *lo = nullptr, *hi = nullptr;
+      c_->comm.share_window(L.win, c_->stream, &lo, &hi, &L.win_ipc);
+      L.win_lo = (char*)lo;
+      L.win_hi = (char*)hi;
+      int tiles = 0, nchunks = 0;
+      fused_shape(L, &tiles, &nchunks);
+      L.peer_tiles = (uint32_t)tiles;
+      L.peer = true;
+    }
+  }
+  // where this rank's sweep into buffer `buf` stores its edge planes: the bottom edge chunk into
+  // rank - 1's mailbox of planes above it (side 1), the top chunk (reflected: plane stride -sz) into
+  // rank + 1's mailbox of planes below it (side 0), filled from its last plane down
+  PeerOut<T> peer_out(const LevelData<T>& L, int buf) const {
+    PeerOut<T> po{{nullptr, nullptr}, {nullptr, nullptr}};
+    if (L.g.zlo_ghost && L.win_lo) {
+      po.dst[0] = mailbox(L.win_lo, L, buf, 1);
+      po.sig[0] = peer_ctl(L.win_lo, L) + buf * 2 + 1;
+    }
+    if (L.g.zhi_ghost && L.win_hi) {
+      po.dst[1] = mailbox(L.win_hi, L, buf, 0) + (int64_t)(GHOST - 1) * L.g.sz;
+      po.sig[1] = peer_ctl(L.win_hi, L) + buf * 2 + 0;
+    }
+    return po;
+  }
+  int buffer_index(const LevelData<T>& L, const T* a) const { return a == L.phys[0] ? 0 : 1; }
+  // x's ghost planes from the neighbours' last peer sweep: wait for their counters, copy the
+  // mailboxes in.  The in-process transport (ranks as threads sharing one device's hardware
+  // queues) waits on the host instead: every rank's stream drained, then a barrier.
+  void peer_resolve(int l) {
+    LevelData<T>& L = lv_[l];
+    if (!L.x_peer_pending) return;
+    L.x_peer_pending = false;
+    const int buf = buffer_index(L, L.x);
+    if (c_->comm.mode() == Comm::LOCAL) c_->comm.local_barrier(c_->stream);
+    const size_t bytes = (size_t)L.ghost * sizeof(T);
+    char* dlo = L.g.zlo_ghost ? (char*)(L.x - L.ghost) : nullptr;
+    char* dhi = L.g.zhi_ghost ? (char*)(L.x + (int64_t)L.g.nz * L.g.sz) : nullptr;
+    const unsigned blocks = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (bytes / 16 + 255) / 256));
+    hipLaunchKernelGGL(peer_unpack_k, dim3(blocks, 2), dim3(256), 0, c_->stream, dlo,
+                       (const char*)mailbox(L.win, L, buf, 0), dhi, (const char*)mailbox(L.win, L, buf, 1),
+                       (uint64_t)bytes, peer_ctl(L.win, L), buf * 2, L.peer_tiles, peer_timeout_ticks_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void peer_resolve_all() {
+    for (size_t l = 0; l < lv_.size(); ++l) peer_resolve((int)l);
+  }
+  // a peer wait that timed out (a neighbour never delivered) is an error, not silent stale halos
+  void peer_check() {
+    for (auto& L : lv_) {
+      if (!L.win) continue;
+      uint32_t err = 0;
+      HIP_CHECK(hipMemcpyAsync(&err, peer_ctl(L.win, L) + 5, sizeof err, hipMemcpyDeviceToHost, c_->stream));
+      HIP_CHECK(hipStreamSynchronize(c_->stream));
+      if (err) throw std::runtime_error("peer halo: a neighbour's edge planes never arrived (wait timed out)");
+    }
   }
 
   // ------------------------------------------------------------- kernel level
@@ -441,6 +551,7 @@ class Solver final : public SolverBase {
   }
 
   void download(int l, int which, double* h) override {
+    peer_check();
     LevelData<T>& L = lv_[l];
     double* tmp = scratch64(L.g.N);
     hipLaunchKernelGGL((convert_k<T, double>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream,
@@ -485,6 +596,7 @@ class Solver final : public SolverBase {
   void halo(int l, T* a, int depth = 1) {
     if (!c_->comm.active() || !c_->geom[l].distributed) return;
     LevelData<T>& L = lv_[l];
+    if (a == L.x && L.x_peer_pending) peer_resolve(l);
     wait_all_pending();
     if (a == L.x && L.x_halo_ok && depth <= GHOST) return;  // ghost planes are current
     c_->comm.exchange_planes(a, L.g.sz, L.g.nz, depth, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(T),
@@ -493,7 +605,11 @@ class Solver final : public SolverBase {
   }
 
   // level l's x changed without its ghost planes (they must be exchanged again)
-  void x_changed(int l) { lv_[l].x_halo_ok = false; }
+  // (a peer batch still in flight for x is taken in first: every batch is consumed exactly once)
+  void x_changed(int l) {
+    if (lv_[l].x_peer_pending) peer_resolve(l);
+    lv_[l].x_halo_ok = false;
+  }
 
   // target grid size of the z-marching transfer kernels
   static constexpr int XFER_BLOCKS = 1024;
@@ -555,10 +671,10 @@ class Solver final : public SolverBase {
     ZRange zr = whole_range(nz, tiles, fc);
     *flip = (c_->d.gs_kernel == 4 && part == 0) ? 1 : 0;
     *sig = nullptr;
-    if (part == 3) {
+    if (part == 3 || part == 4) {
       REQUIRE(zr.nchunks >= 2 && zr.zc >= GHOST, MAD_ERR_UNSUPPORTED, "slab too thin for the single-launch sweep");
       *flip = 1;
-      *sig = L.sig;
+      *sig = part == 3 ? L.sig : nullptr;
     } else if (part == 1) {
       zr = ZRange{0, boundary_planes(), nz - boundary_planes(), 2};
     } else if (part == 2) {
@@ -586,6 +702,7 @@ class Solver final : public SolverBase {
     // fp64 doubles the register footprint: 2 waves per SIMD (one 512-thread block per CU,
     // which is all its LDS allows anyway)
     constexpr int MW = sizeof(T) == 8 ? 2 : 4;
+    const PeerOut<T> po = part == 4 ? peer_out(L, buffer_index(L, L.t)) : PeerOut<T>{{nullptr, nullptr}, {nullptr, nullptr}};
     auto run = [&](auto kern) {
       // every instance that can be launched gets its dynamic-LDS opt-in (a kernel pointer
       // set, not one flag per function type: several instances share one signature)
@@ -596,12 +713,18 @@ class Solver final : public SolverBase {
         attr.push_back((const void*)kern);
       }
       hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig);
+                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, po);
     };
-    if (L.brec)
+    if (part == 4) {
+      if (L.brec)
+        run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true, true>);
+      else
+        run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>);
+    } else if (L.brec) {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
-    else
+    } else {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+    }
   }
 
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
@@ -636,7 +759,7 @@ class Solver final : public SolverBase {
     if (c_->d.smoother == MAD_WEIGHTED_JACOBI) {
       const LevelData<T>& L = lv_[l];
       if (dim == 3 && L.g.nx >= 16 && L.g.ny >= 16)
-        std::snprintf(buf, sizeof buf, "wj3_k<%s, %d, 64, 16%s>", tn, kind, L.brec ? ", true" : "");
+        std::snprintf(buf, sizeof buf, "wj3_k<%s, %d, 64, 16, %s>", tn, kind, L.brec ? "true" : "false");
       else
         std::snprintf(buf, sizeof buf, "wj_k<%s, %d, %d>", tn, dim, kind);
     } else if (c_->d.smoother == MAD_GAUSS_SEIDEL_LEX) {
@@ -647,11 +770,12 @@ class Solver final : public SolverBase {
       const int tx = 64, ty = (kind == KFULL && sizeof(T) == 4) ? 32 : 16;
       const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : 1024;
       const bool brec = lv_[l].brec;
-      // every template argument, as rocprofv3 prints the instantiation (BREC last)
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s>", tn, kind, tx, ty, nt,
-                    sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false");
-      // rank slabs: which sweep form fused_sweep takes
       const LevelData<T>& L = lv_[l];
+      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER last)
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s>", tn, kind, tx, ty, nt,
+                    sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false", L.peer ? "true" : "false");
+      // rank slabs: which sweep form fused_sweep takes
+      if (L.peer) return std::string(buf) + " [rank slab: peer halo, edge planes stored by the sweep]";
       if (sweep_overlap(l)) {
         int tiles = 0, nchunks = 0;
         fused_shape(L, &tiles, &nchunks);
@@ -723,6 +847,16 @@ class Solver final : public SolverBase {
       L.b_halo_ok = true;
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
+    if (L.peer) {
+      // the sweep delivers its edge planes to the neighbours itself; no exchange follows
+      launch_fused_part(L, 4);
+      if (e1) HIP_CHECK(hipEventRecord(e1, c_->stream));
+      std::swap(L.x, L.t);
+      std::swap(L.alloc[0], L.alloc[3]);
+      L.x_halo_ok = true;
+      L.x_peer_pending = true;
+      return 0.f;
+    }
     const bool overlap = sweep_overlap(l);
     int tiles = 0, nchunks = 0;
     if (overlap) fused_shape(L, &tiles, &nchunks);
@@ -1238,6 +1372,7 @@ class Solver final : public SolverBase {
   // canonical entry state of a multi-rank graph cycle (host bookkeeping + level 0's
   // ghost planes made current on the stream)
   void ranks_graph_entry() {
+    peer_resolve_all();
     halo(0, lv_[0].x, GHOST);
     if (!lv_[0].brec && !lv_[0].b_halo_ok) {
       halo(0, lv_[0].b, GHOST);
@@ -1303,7 +1438,10 @@ class Solver final : public SolverBase {
       bool captured = true;
       try {
         vcycle_rec(0);
-        if (ranks) wait_all_pending();  // join the communication stream: no open branch
+        if (ranks) {
+          wait_all_pending();  // join the communication stream: no open branch
+          peer_resolve_all();  // and no peer batch left to take in
+        }
       } catch (...) {
         (void)hipStreamEndCapture(c_->stream, &gph);
         if (gph) (void)hipGraphDestroy(gph);
@@ -1734,6 +1872,7 @@ class Solver final : public SolverBase {
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
   std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
   bool vgraph_failed_ = false;
+  uint64_t peer_timeout_ticks_ = 0;
   std::vector<HaloFlags> vgraph_exit_flags_;  // rank slabs: ghost bookkeeping after one cycle
   int vcycles_eager_ = 0;  // rank slabs: cycles run eagerly so far (RCCL peers connected)
   int ncoef_ = 0;
@@ -1760,6 +1899,9 @@ class Solver final : public SolverBase {
       if (L.ev_bnd) (void)hipEventDestroy(L.ev_bnd);
       if (L.ev_halo) (void)hipEventDestroy(L.ev_halo);
       if (L.sig) (void)hipFree(L.sig);
+      Comm::close_window(L.win_lo, L.win_ipc);
+      Comm::close_window(L.win_hi, L.win_ipc);
+      if (L.win) (void)hipFree(L.win);
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
@@ -2340,7 +2482,8 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             "bad rank / nranks");
     REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
-    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP)) == 0, MAD_ERR_INVALID, "unknown option bits");
+    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO)) == 0,
+            MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
     REQUIRE(d->coarse_dense_max >= 0 && d->coarse_dense_max <= 65536, MAD_ERR_INVALID,

@@ -59,9 +59,17 @@ def pytest_sessionstart(session):
     config = session.config
     if not _gpu_selected(config) or os.environ.get("MAD_SKIP_MULTIPROC"):
         return
-    world = min(_count_gpus(), 8)
+    ngpu = _count_gpus()
+    world, shared = min(ngpu, 8), False
     if world < 2:
-        return
+        if ngpu < 1 or os.environ.get("MAD_SKIP_SHARED_MULTIPROC"):
+            return
+        # one GPU: two RCCL rank processes share it.  RCCL refuses two ranks of one
+        # communicator on one device of one host ("Duplicate GPU"); a distinct NCCL_HOSTID per
+        # rank makes them two hosts to RCCL, so they connect over its socket transport
+        # (loopback) -- real two-process RCCL (bootstrap, grouped send/recv, allreduce,
+        # allgather, graph-captured V-cycles), with host-staged bytes instead of xGMI.
+        world, shared = 2, True
     outdir = tempfile.mkdtemp(prefix="mad_mp_")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                WORLD_SIZE=str(world))
@@ -69,13 +77,19 @@ def pytest_sessionstart(session):
     procs, logs = [], []
     for r in range(world):
         log = os.path.join(outdir, f"rank{r}.log")
+        renv = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        if shared:
+            # INFO on the INIT / NET subsystems: the log names the transport RCCL connected
+            # the two ranks with (the test checks it is the network one, NET/Socket)
+            renv.update(MAD_MP_DEVICE="0", NCCL_HOSTID=f"mad-shared-gpu-rank{r}",
+                        NCCL_IB_DISABLE="1", NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,NET")
         with open(log, "w") as f:
             procs.append(subprocess.Popen(
                 [sys.executable, os.path.join(ROOT, "tests", "mp_rank.py"), outdir],
-                env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=f, stderr=subprocess.STDOUT,
+                env=renv, stdout=f, stderr=subprocess.STDOUT,
                 cwd=ROOT, start_new_session=True))
         logs.append(log)
-    _MP["job"] = dict(procs=procs, logs=logs, outdir=outdir, world=world)
+    _MP["job"] = dict(procs=procs, logs=logs, outdir=outdir, world=world, shared=shared)
 
 
 def pytest_collection_modifyitems(session, config, items):

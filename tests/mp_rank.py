@@ -31,11 +31,18 @@ def drive(s, M):
     return out
 
 
-def make_solver(M, world, rank, device=-1):
+def variants(M):
+    """(name, mad_desc.options) of the sequences every rank runs: the default exchange after
+    each sweep (RCCL grouped send / recv), and the peer halo (edge planes stored by the sweep
+    into the neighbours' IPC-mapped mailboxes)."""
+    return [("default", 0), ("peer", M.capi.OPT_PEER_HALO)]
+
+
+def make_solver(M, world, rank, device=-1, options=0):
     from multigridanisotropicdiffusion_amd import distributed as D
     z0, z1 = D.slabs(GSHAPE, world)[rank]
     return M.Solver((z1 - z0,) + GSHAPE[1:], time_step=0.1, precision=M.FP32, cycle=M.VCYCLE,
-                    nranks=world, rank=rank, global_shape=GSHAPE, device=device)
+                    nranks=world, rank=rank, global_shape=GSHAPE, device=device, options=options)
 
 
 def main():
@@ -43,15 +50,18 @@ def main():
     from multigridanisotropicdiffusion_amd import distributed as D
     outdir = sys.argv[1]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    s = make_solver(M, world, rank, device=rank)
-    D.bootstrap_node(s, rank, world, tag="mp_parity")
-    s.synth_tensor(kind=0, seed=4)
-    s.setup()
-    out = drive(s, M)
-    out["kernel"] = np.array(s.smooth_kernel_name(0))
-    s.close()
-    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
-    print(f"rank {rank}/{world}: done", flush=True)
+    # MAD_MP_DEVICE: the shared-device mode of tests/conftest.py (both ranks on GPU 0)
+    device = int(os.environ.get("MAD_MP_DEVICE", rank))
+    for name, opts in variants(M):
+        s = make_solver(M, world, rank, device=device, options=opts)
+        D.bootstrap_node(s, rank, world, tag=f"mp_parity_{name}")
+        s.synth_tensor(kind=0, seed=4)
+        s.setup()
+        out = drive(s, M)
+        out["kernel"] = np.array(s.smooth_kernel_name(0))
+        s.close()
+        np.savez(os.path.join(outdir, f"rank{rank}_{name}.npz"), **out)
+        print(f"rank {rank}/{world} {name}: done", flush=True)
 
 
 if __name__ == "__main__":

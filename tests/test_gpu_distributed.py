@@ -37,12 +37,13 @@ def _multi(nranks, fn, T, **kw):
 @pytest.mark.parametrize("nranks", [2, 4])
 @pytest.mark.parametrize("smoother,gs_kernel,cycle,options", [(0, 0, 0, 0), (0, 1, 0, 0), (2, 0, 0, 0),
                                                               (0, 3, 0, 0), (0, 3, 2, 0), (0, 3, 0, 2),
-                                                              (0, 3, 2, 2)])
+                                                              (0, 3, 2, 2), (0, 3, 0, 4), (0, 3, 2, 4)])
 def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle, options):
     """cycle 2 (SMOOTHER): level-0 records carry b (sync_brec on ghost planes).  gs_kernel 3 forces
     the fused sweep on these small levels, in its default serial rank form (one launch, then the
     exchange) or with options 2 (MAD_OPT_OVERLAP_RANK_SWEEP) in the split form (boundary chunks,
-    exchange beside the interior launch)."""
+    exchange beside the interior launch), or with options 4 (MAD_OPT_PEER_HALO: the sweep stores its
+    edge planes into the neighbours' mailboxes; 2 ranks, where the 32-plane slabs make two z-chunks)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     T = synth.random_spd(SHAPE, seed=3)
@@ -218,7 +219,8 @@ def test_solo_transport_times_one_rank():
         s.close()
 
 
-@pytest.mark.parametrize("cycle,gs_kernel,overlap", [(0, 0, 0), (2, 0, 0), (0, 3, 0), (0, 3, 1)])
+@pytest.mark.parametrize("cycle,gs_kernel,overlap", [(0, 0, 0), (2, 0, 0), (0, 3, 0), (0, 3, 1), (0, 3, 4),
+                                                     (2, 3, 4)])
 def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     """The multi-rank V-cycle replays a captured hipGraph on RCCL / SOLO ranks (host bookkeeping
     of which ghost planes are current decides what the graph re-exchanges).  On the SOLO
@@ -226,13 +228,15 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     several V-cycles, an odd sweep count in between (the ping-pong parity flips), more
     V-cycles -- equals the eager execution (mad_desc.options MAD_OPT_EAGER_RANK_VCYCLE) bit for
     bit on every level's x and b; gs_kernel 3 puts the fused rank sweep into the graph, serial
-    (the default) or split (MAD_OPT_OVERLAP_RANK_SWEEP: a communication-stream branch)."""
+    (the default), split (MAD_OPT_OVERLAP_RANK_SWEEP: a communication-stream branch) or with the
+    peer halo (MAD_OPT_PEER_HALO: edge planes into the rank's own stand-in mailboxes, the unpack
+    launch waiting on its counters inside the graph)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     shape = (128, 64, 64)
     z0, z1 = D.slabs(shape, 4)[2]
     out = {}
-    base = M.capi.OPT_OVERLAP_RANK_SWEEP if overlap else 0
+    base = {0: 0, 1: M.capi.OPT_OVERLAP_RANK_SWEEP, 4: M.capi.OPT_PEER_HALO}[overlap]
     for opt in (0, M.capi.OPT_EAGER_RANK_VCYCLE):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
                      global_shape=shape, min_slab_voxels=DEEP, options=opt | base, gs_kernel=gs_kernel)
@@ -257,8 +261,8 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
         np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")
 
 
-@pytest.mark.parametrize("cycle,gs_kernel", [(0, 0), (0, 3), (2, 3)])
-def test_rccl_solo_equals_solo(cycle, gs_kernel):
+@pytest.mark.parametrize("cycle,gs_kernel,options", [(0, 0, 0), (0, 3, 0), (2, 3, 0), (0, 3, 4)])
+def test_rccl_solo_equals_solo(cycle, gs_kernel, options):
     """mad_comm_init_rccl_solo moves SOLO's bytes through RCCL (a single-rank communicator, every
     grouped exchange ncclSend / ncclRecv pairs to itself, inside the captured V-cycle graph too):
     the same sequence -- partitioned setup (hop-by-hop tensor ghost planes), sweeps, graph-replayed
@@ -270,7 +274,7 @@ def test_rccl_solo_equals_solo(cycle, gs_kernel):
     out = {}
     for mode in ("solo", "rccl"):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
-                     global_shape=shape, min_slab_voxels=DEEP, gs_kernel=gs_kernel)
+                     global_shape=shape, min_slab_voxels=DEEP, gs_kernel=gs_kernel, options=options)
         if mode == "solo":
             s.comm_init_solo()
         else:

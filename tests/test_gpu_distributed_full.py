@@ -30,17 +30,24 @@ def _drive(s, M):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("gshape,nranks,cycle", [
-    ((512, 512, 512), 2, 0),
-    ((512, 512, 512), 4, 0),
-    ((512, 512, 512), 8, 0),
-    ((512, 512, 512), 8, 2),        # SMOOTHER layout (records carry b): the bench's sweep
-    ((512, 1024, 1024), 8, 0),      # C5
+@pytest.mark.parametrize("gshape,nranks,cycle,peer", [
+    ((512, 512, 512), 2, 0, 0),
+    ((512, 512, 512), 4, 0, 0),
+    ((512, 512, 512), 8, 0, 0),
+    ((512, 512, 512), 8, 2, 0),     # SMOOTHER layout (records carry b): the bench's sweep
+    ((512, 1024, 1024), 8, 0, 0),   # C5
+    # MAD_OPT_PEER_HALO: the fused sweeps store their edge planes into the neighbours' mailboxes
+    ((512, 512, 512), 2, 0, 1),
+    ((512, 512, 512), 4, 0, 1),
+    ((512, 512, 512), 8, 0, 1),
+    ((512, 512, 512), 8, 2, 1),
 ])
-def test_full_size_slabs_bitwise(gshape, nranks, cycle):
+def test_full_size_slabs_bitwise(gshape, nranks, cycle, peer):
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
-    opts = M.capi.OPT_OVERLAP_RANK_SWEEP if cycle == 2 else 0
+    opts = M.capi.OPT_OVERLAP_RANK_SWEEP if cycle == 2 and not peer else 0
+    if peer:
+        opts |= M.capi.OPT_PEER_HALO
     kw = dict(time_step=0.1, precision=M.FP32, cycle=cycle, gs_kernel=0, options=opts)
     s = M.Solver(gshape, **kw)
     s.synth_tensor(kind=0, seed=4)
@@ -61,6 +68,7 @@ def test_full_size_slabs_bitwise(gshape, nranks, cycle):
     out = D.run_local(nranks, body, gshape, **kw)
     sl = D.slabs(gshape, nranks)
     for r, ((a, v), kname) in enumerate(out):
+        assert ("peer halo" in kname) == bool(peer), kname
         z0, z1 = sl[r]
         assert z1 - z0 == gshape[0] // nranks
         np.testing.assert_array_equal(a, ref[0][z0:z1], err_msg=f"rank {r} sweeps ({kname})")

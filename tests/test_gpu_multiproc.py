@@ -1,11 +1,20 @@
 """Multi-process RCCL parity (one process per GPU, the driver's multi-GPU layout).
 
 tests/conftest.py starts N = min(visible GPUs, 8) rank processes (tests/mp_rank.py) at session
-start, before this process touches a GPU, when the gpu tests are selected and >= 2 GPUs are
-visible; here they are joined and their rank slabs compared BIT for bit with the same sequence
-on the in-process LOCAL transport (ranks as threads on one device; itself bitwise equal to the
-single-rank run, test_gpu_distributed_full.py): two level-0 sweeps and three V-cycles at 512^3,
-the later ones replaying the captured multi-rank hipGraph over RCCL.  One visible GPU: skipped.
+start, before this process touches a GPU, when the gpu tests are selected; here they are joined
+and their rank slabs compared BIT for bit with the same sequence on the in-process LOCAL
+transport (ranks as threads on one device; itself bitwise equal to the single-rank run,
+test_gpu_distributed_full.py): two level-0 sweeps and three V-cycles at 512^3, the later ones
+replaying the captured multi-rank hipGraph over RCCL -- once with the default exchange (grouped
+ncclSend / ncclRecv after each sweep) and once with MAD_OPT_PEER_HALO (the sweep stores its edge
+planes into the neighbours' mailboxes, mapped across the processes with hipIpc handles).
+
+With one visible GPU, two rank processes share it: a distinct NCCL_HOSTID per rank makes them
+two hosts to RCCL (whose duplicate-GPU check refuses two ranks of one device on one host), so
+they connect over RCCL's socket transport on loopback -- a real two-process RCCL run (bootstrap,
+grouped send / recv, allreduce, allgather, graph capture) with host-staged bytes instead of
+xGMI, and the peer halo's IPC mapping between two processes (on one device, so its cross-GPU
+memory ordering is not exercised there).
 """
 import os
 
@@ -20,11 +29,22 @@ def test_rccl_rank_processes_equal_local_transport(pytestconfig):
     import conftest
     job = conftest.multiproc_job(pytestconfig)
     if job is None:
-        pytest.skip("needs >= 2 visible GPUs (one RCCL rank process per GPU)")
+        pytest.skip("no GPU visible, or MAD_SKIP_MULTIPROC / MAD_SKIP_SHARED_MULTIPROC set")
     rcs = conftest.join_multiproc(job, timeout=420)
-    logs = {r: open(job["logs"][r]).read()[-2000:] for r in range(job["world"])}
+    full = {r: open(job["logs"][r]).read() for r in range(job["world"])}
+    logs = {r: full[r][-2000:] for r in range(job["world"])}
+    keep = os.environ.get("MAD_MP_KEEP_LOGS")
+    if keep:  # evidence runs: the rank logs next to the other results
+        os.makedirs(keep, exist_ok=True)
+        for r in range(job["world"]):
+            with open(os.path.join(keep, f"mp_rank{r}.log"), "w") as f:
+                f.write(full[r])
     for r, rc in enumerate(rcs):
         assert rc == 0, f"rank {r} exited {rc}:\n{logs[r]}"
+    if job.get("shared"):
+        # the two ranks of the shared GPU really exchanged through RCCL's network transport
+        for r in range(job["world"]):
+            assert "via NET/Socket" in full[r], f"rank {r}: no NET/Socket channel in its log\n{logs[r]}"
 
     import mp_rank
     import multigridanisotropicdiffusion_amd as M
@@ -36,9 +56,12 @@ def test_rccl_rank_processes_equal_local_transport(pytestconfig):
         s.setup()
         return mp_rank.drive(s, M)
 
-    ref = D.run_local(world, body, mp_rank.GSHAPE, time_step=0.1, precision=M.FP32, cycle=M.VCYCLE)
-    for r in range(world):
-        with np.load(os.path.join(job["outdir"], f"rank{r}.npz"), allow_pickle=False) as z:
-            got = {k: z[k] for k in z.files}
-        for k, v in ref[r].items():
-            np.testing.assert_array_equal(got[k], v, err_msg=f"rank {r} {k} ({got['kernel']})")
+    for name, opts in mp_rank.variants(M):
+        ref = D.run_local(world, body, mp_rank.GSHAPE, time_step=0.1, precision=M.FP32, cycle=M.VCYCLE,
+                          options=opts)
+        for r in range(world):
+            with np.load(os.path.join(job["outdir"], f"rank{r}_{name}.npz"), allow_pickle=False) as z:
+                got = {k: z[k] for k in z.files}
+            assert ("peer halo" in str(got["kernel"])) == (name == "peer"), got["kernel"]
+            for k, v in ref[r].items():
+                np.testing.assert_array_equal(got[k], v, err_msg=f"{name}: rank {r} {k} ({got['kernel']})")
