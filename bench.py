@@ -48,6 +48,10 @@ def parse():
     p.add_argument("--cpu-size", type=int, default=0,
                    help="volume of the CPU baseline (default: the benched size)")
     p.add_argument("--no-precision-cycles", action="store_true")
+    p.add_argument("--halo", default="peer", choices=["peer", "rccl"],
+                   help="rank slabs (N > 1): 'peer' -- the fused level-0 sweep stores its edge planes "
+                        "into the neighbours' mailboxes while it runs (MAD_OPT_PEER_HALO); 'rccl' -- a "
+                        "grouped ncclSend / ncclRecv exchange after each sweep")
     return p.parse_args()
 
 
@@ -186,6 +190,14 @@ def main():
     # ROCm RCCL it was compiled against (torch would bring its own librccl.so.1 first).
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_DEBUG", "WARN")
+    # MAD_BENCH_SHARED_GPU=1 (rehearsal of the N > 1 launch on a one-GPU box): every rank on
+    # device 0, a distinct NCCL_HOSTID per rank so RCCL accepts two ranks of one device (it
+    # connects them over its socket transport); the timings then measure nothing about xGMI
+    shared_gpu = world > 1 and os.environ.get("MAD_BENCH_SHARED_GPU") == "1"
+    if shared_gpu:
+        os.environ["NCCL_HOSTID"] = f"mad-bench-rank{rank}"
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        local = 0
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as MD
 
@@ -194,12 +206,13 @@ def main():
     nz_local = S // world
     shape = (nz_local, S, S)
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
+    opts = M.capi.OPT_PEER_HALO if (world > 1 and a.halo == "peer") else 0
     # SMOOTHER mode (the reference's CycleType 2: repeated sweeps of one system) -- the
     # smoother-only protocol of SURVEY §8(d); level-0 records then carry b (mad_solver.hip)
     s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
                  cycle=M.SMOOTHER,
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
-                 gs_kernel=a.gs_kernel)
+                 gs_kernel=a.gs_kernel, options=opts)
     if world > 1:
         MD.bootstrap_node(s, rank, world, tag="sweep")
     s.synth_tensor(kind=0, seed=4)
@@ -241,7 +254,7 @@ def main():
     s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
                  cycle=M.VCYCLE,
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
-                 gs_kernel=a.gs_kernel)
+                 gs_kernel=a.gs_kernel, options=opts)
     if world > 1:
         MD.bootstrap_node(s, rank, world, tag="vcycle")
     s.synth_tensor(kind=0, seed=4)
@@ -293,11 +306,15 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (device-generated VED-form tensor and counter-hash image)",
+        "data": "synthetic (device-generated VED-form tensor and counter-hash image)"
+                + ("; REHEARSAL: all ranks share GPU 0 (MAD_BENCH_SHARED_GPU)" if shared_gpu else ""),
         "config": {"workload": f"C4 {S}^3 VED-form full tensor, "
                                f"{'4-colour Gauss-Seidel' if a.smoother == 'gs' else 'weighted Jacobi'}"
                                f" level-0 sweeps", "global_shape": list(gshape),
                    "levels": nlev, "time_step": 0.1, "parallelism": f"z-slab x{world}",
+                   "halo": (None if world == 1 else
+                            ("peer: edge planes stored by the sweep into the neighbours' mailboxes"
+                             if "peer halo" in kname else "rccl: grouped send/recv after each sweep")),
                    "slab_shape": list(info["shape"])},
         "vcycles_per_s": round(a.vcycles / vwall, 3),
         "vcycle_config": "CycleType VCYCLE (dense rhs layout), nu = 2, 4-colour GS, "

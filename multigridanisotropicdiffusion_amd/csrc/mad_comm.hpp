@@ -234,6 +234,8 @@ class Comm {
   }
 
   bool active() const { return mode_ != NONE && nranks_ > 1; }
+  // SOLO / RCCL-SOLO: the rank's own arrays stand in for its neighbours'
+  bool stand_in() const { return mode_ == SOLO || (mode_ == RCCL && self_); }
   // RCCL peer of neighbour rank q (RCCL-SOLO: every peer is this process's only rank)
   int peer(int q) const { return self_ ? 0 : (q + nranks_) % nranks_; }
   Mode mode() const { return mode_; }
@@ -493,14 +495,52 @@ class Comm {
     HIPC_CHECK(hipMemcpyAsync(all.data(), d, hb * nranks_, hipMemcpyDeviceToHost, s));
     HIPC_CHECK(hipStreamSynchronize(s));
     HIPC_CHECK(hipFree(d));
+    // a neighbour's window this process cannot map (no peer access between the two GPUs) makes
+    // every rank give the windows up together -- the caller falls back to the exchange -- instead
+    // of one rank throwing while the others wait in their next collective
+    bool ok = true;
     auto open = [&](int r, void** p) {
       hipIpcMemHandle_t h;
       std::memcpy(&h, all.data() + hb * r, hb);
-      HIPC_CHECK(hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess));
+      if (hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        ok = false;
+      }
     };
     if (rank_ > 0) open(rank_ - 1, lo);
     if (rank_ < nranks_ - 1) open(rank_ + 1, hi);
     *ipc = true;
+    if (!all_true(ok, s)) {
+      close_window(*lo, true);
+      close_window(*hi, true);
+      *lo = *hi = nullptr;
+      *ipc = false;
+    }
+  }
+
+  // logical AND of one flag over the ranks (collective)
+  bool all_true(bool v, hipStream_t s) {
+    if (mode_ == RCCL && !self_) {
+      int32_t* d = nullptr;
+      int32_t h = v ? 1 : 0;
+      HIPC_CHECK(hipMalloc(&d, sizeof(int32_t)));
+      HIPC_CHECK(hipMemcpyAsync(d, &h, sizeof h, hipMemcpyHostToDevice, s));
+      NCCL_CHECK(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, comm_, s));
+      HIPC_CHECK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, s));
+      HIPC_CHECK(hipStreamSynchronize(s));
+      HIPC_CHECK(hipFree(d));
+      return h != 0;
+    }
+    if (mode_ == LOCAL) {
+      group_->val[rank_] = v ? 1.0 : 0.0;
+      group_->barrier();
+      bool all = true;
+      for (int r = 0; r < nranks_; ++r) all = all && group_->val[r] != 0.0;
+      group_->barrier();
+      return all;
+    }
+    return v;
   }
   static void close_window(void* p, bool ipc) {
     if (p && ipc) (void)hipIpcCloseMemHandle(p);

@@ -765,12 +765,19 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
           }
           if (signals && mo == GHOST - 1) {
             // the edge planes 0..GHOST-1 of this tile are stored: release them, count in
-            if (PEER)
-              __threadfence_system();
-            else
+            if (PEER) {
+              // the mailbox and the counters are uncached memory (no L2 on either GPU holds them):
+              // once every thread's mailbox stores have completed (vmcnt 0) the tile is counted
+              // in.  A system-scope release fence here would write back the whole L2 (full of
+              // this sweep's dirty output) once per tile: 0.30 vs 0.20 ms per 64-plane rank sweep
+              __builtin_amdgcn_s_waitcnt(0);
+              __syncthreads();
+              if (tid == 0) __hip_atomic_fetch_add(psig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
               __threadfence();
-            __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add(psig, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+              __syncthreads();
+              if (tid == 0) __hip_atomic_fetch_add(psig, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
           }
         }
       }

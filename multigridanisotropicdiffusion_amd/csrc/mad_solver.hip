@@ -476,6 +476,13 @@ class Solver final : public SolverBase {
       c_->comm.share_window(L.win, c_->stream, &lo, &hi, &L.win_ipc);
       L.win_lo = (char*)lo;
       L.win_hi = (char*)hi;
+      if ((L.g.zlo_ghost && !lo) || (L.g.zhi_ghost && !hi)) {
+        // the windows could not be mapped on every rank (share_window agreed on it): this level
+        // exchanges after its sweeps as without the option
+        HIP_CHECK(hipFree(L.win));
+        L.win = nullptr;
+        continue;
+      }
       int tiles = 0, nchunks = 0;
       fused_shape(L, &tiles, &nchunks);
       L.peer_tiles = (uint32_t)tiles;
@@ -485,15 +492,22 @@ class Solver final : public SolverBase {
   // where this rank's sweep into buffer `buf` stores its edge planes: the bottom edge chunk into
   // rank - 1's mailbox of planes above it (side 1), the top chunk (reflected: plane stride -sz) into
   // rank + 1's mailbox of planes below it (side 0), filled from its last plane down
+  // SOLO / RCCL-SOLO (the own window stands in for both neighbours): each edge chunk fills the
+  // own mailbox of its own side, as SOLO's exchange copies the own edge planes into the own ghost
+  // planes -- the same bytes, and a rank at either end of the decomposition waits only on the side
+  // it has
   PeerOut<T> peer_out(const LevelData<T>& L, int buf) const {
     PeerOut<T> po{{nullptr, nullptr}, {nullptr, nullptr}};
+    const bool self = c_->comm.stand_in();
     if (L.g.zlo_ghost && L.win_lo) {
-      po.dst[0] = mailbox(L.win_lo, L, buf, 1);
-      po.sig[0] = peer_ctl(L.win_lo, L) + buf * 2 + 1;
+      const int side = self ? 0 : 1;
+      po.dst[0] = mailbox(L.win_lo, L, buf, side);
+      po.sig[0] = peer_ctl(L.win_lo, L) + buf * 2 + side;
     }
     if (L.g.zhi_ghost && L.win_hi) {
-      po.dst[1] = mailbox(L.win_hi, L, buf, 0) + (int64_t)(GHOST - 1) * L.g.sz;
-      po.sig[1] = peer_ctl(L.win_hi, L) + buf * 2 + 0;
+      const int side = self ? 1 : 0;
+      po.dst[1] = mailbox(L.win_hi, L, buf, side) + (int64_t)(GHOST - 1) * L.g.sz;
+      po.sig[1] = peer_ctl(L.win_hi, L) + buf * 2 + side;
     }
     return po;
   }
@@ -510,6 +524,8 @@ class Solver final : public SolverBase {
     const size_t bytes = (size_t)L.ghost * sizeof(T);
     char* dlo = L.g.zlo_ghost ? (char*)(L.x - L.ghost) : nullptr;
     char* dhi = L.g.zhi_ghost ? (char*)(L.x + (int64_t)L.g.nz * L.g.sz) : nullptr;
+    // at most 2 x 64 workgroups: while they wait, the other CUs stay free for a neighbour's sweep
+    // that shares the device (the one-GPU two-process test; LOCAL ranks wait on the host)
     const unsigned blocks = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (bytes / 16 + 255) / 256));
     hipLaunchKernelGGL(peer_unpack_k, dim3(blocks, 2), dim3(256), 0, c_->stream, dlo,
                        (const char*)mailbox(L.win, L, buf, 0), dhi, (const char*)mailbox(L.win, L, buf, 1),

@@ -295,3 +295,29 @@ def test_rccl_solo_equals_solo(cycle, gs_kernel, options):
         assert np.isfinite(xa).all()
         np.testing.assert_array_equal(xa, xb, err_msg=f"x, level {l}")
         np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")
+
+
+@pytest.mark.parametrize("rank", [0, 3])
+def test_solo_peer_halo_end_ranks(rank):
+    """MAD_OPT_PEER_HALO on a rank at either end of the decomposition (one neighbour): on the SOLO
+    transport its edge chunk fills its own stand-in mailbox of the side it has, so every unpack's
+    wait is met -- sweeps, graph-replayed V-cycles and the download's peer check finish (a wait
+    that timed out would raise there)."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    shape = (128, 64, 64)
+    z0, z1 = D.slabs(shape, 4)[rank]
+    for cycle in (0, 2):
+        s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=rank,
+                     global_shape=shape, min_slab_voxels=DEEP, options=M.capi.OPT_PEER_HALO, gs_kernel=3)
+        s.comm_init_solo()
+        s.synth_tensor(kind=0, seed=9)
+        s.setup()
+        assert "peer halo" in s.smooth_kernel_name(0)
+        s.synth_level(0, M.capi.B, 3)
+        s.synth_level(0, M.capi.X, 4)
+        s.smooth(0, 3)
+        for _ in range(3):
+            s.vcycle()
+        assert np.isfinite(s.download(0, M.capi.X)).all()
+        s.close()
