@@ -175,6 +175,15 @@ def load_traffic(tag, kernel_sig):
     return None
 
 
+T0 = time.perf_counter()
+
+
+def phase(rank, what):
+    """One progress line per phase on stderr (the JSON line alone goes to stdout): a run that
+    stops shows where, on every rank."""
+    print(f"[bench rank {rank} +{time.perf_counter() - T0:7.1f} s] {what}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,7 +223,9 @@ def main():
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
                  gs_kernel=a.gs_kernel, options=opts)
     if world > 1:
+        phase(rank, "sweep solver: joining the communicator")
         MD.bootstrap_node(s, rank, world, tag="sweep")
+    phase(rank, "sweep solver: setup")
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
@@ -226,6 +237,7 @@ def main():
         if world > 1:
             s.allreduce([0.0])
 
+    phase(rank, f"sweeps: {a.warmup} warmup + {a.steps} timed ({s.smooth_kernel_name(0)})")
     # warmup
     if a.warmup:
         s.bench_smooth(0, a.warmup)
@@ -240,6 +252,7 @@ def main():
     # beside the contract's K steps (24 ms at K = 20): a sustained window of ~2 s of the same
     # sweeps, device-timed, so the rate is also measured over a span a utilisation sampler sees
     sus_n = max(a.steps, int(2000.0 / max(wall / a.steps * 1e3, 0.05)))
+    phase(rank, f"sweeps: sustained window of {sus_n}")
     sus_dev, sus_kern, _ = s.bench_smooth(0, sus_n)
     if world > 1:
         sus_dev = float(s.allreduce([sus_dev], "max")[0])
@@ -256,7 +269,9 @@ def main():
                  nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
                  gs_kernel=a.gs_kernel, options=opts)
     if world > 1:
+        phase(rank, "V-cycle solver: joining the communicator")
         MD.bootstrap_node(s, rank, world, tag="vcycle")
+    phase(rank, "V-cycle solver: setup")
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
@@ -264,6 +279,7 @@ def main():
     s.vcycle()
     barrier()
     t1 = time.perf_counter()
+    phase(rank, f"V-cycles: {a.vcycles} timed")
     vc_ms = s.bench_vcycle(a.vcycles)
     barrier()
     vwall = time.perf_counter() - t1
@@ -333,6 +349,7 @@ def main():
         # arithmetic throughout), beside the plain fp32 cycle of the same loop
         pc = {}
         for key, prec in (("fp32", M.FP32), ("refine", M.FP32_REFINE), ("fp64", M.FP64)):
+            phase(rank, f"mad_run cycle cost: {key}")
             pc[key] = run_cycle_ms(M, gshape, prec, 8, smoother=sm, gs_kernel=a.gs_kernel)
         line["run_ms_per_cycle"] = {k: round(v, 3) for k, v in pc.items()}
         line["refine_vcycles_per_s"] = round(1e3 / pc["refine"], 2)
@@ -342,6 +359,7 @@ def main():
                                     "refine = MAD_FP32_REFINE, what MAD_PRECISION_AUTO resolves to at "
                                     "the reference tests' 1e-10")
     if world == 1 and not a.no_cpu_baseline:
+        phase(rank, "CPU baseline (oracle)")
         cb = cpu_baseline(a.cpu_seconds, a.cpu_size or S)
         line["cpu_baseline"] = cb
     else:
