@@ -224,6 +224,9 @@ class Comm {
   }
 
   void destroy() {
+    if (graph_pending_ && graph_stream_) (void)hipStreamSynchronize(graph_stream_);
+    graph_pending_ = false;
+    graph_stream_ = nullptr;
     if (comm_) (void)ncclCommDestroy(comm_);
     comm_ = nullptr;
     group_.reset();
@@ -234,6 +237,28 @@ class Comm {
   }
 
   bool active() const { return mode_ != NONE && nranks_ > 1; }
+
+  // A captured graph holding RCCL operations posts their proxy work when the device reaches
+  // them, an eager RCCL call when it is enqueued: an eager call issued while such a graph is still
+  // in flight can reach the proxy ahead of the graph's operations on one rank and behind them on
+  // another, and the ranks' send / recv pairs no longer match (seen on two rank processes over the
+  // socket transport as "message truncated", then a hang).  So the solver marks every launch of
+  // such a graph, and the next eager RCCL call first waits for it (settle); calls being captured
+  // are only recorded and need no wait.
+  void graph_launched(hipStream_t s) {
+    if (mode_ == RCCL) {
+      graph_stream_ = s;
+      graph_pending_ = true;
+    }
+  }
+  void settle(hipStream_t s) {
+    if (!graph_pending_) return;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    HIPC_CHECK(hipStreamIsCapturing(s, &st));
+    if (st != hipStreamCaptureStatusNone) return;
+    HIPC_CHECK(hipStreamSynchronize(graph_stream_));
+    graph_pending_ = false;
+  }
   // SOLO / RCCL-SOLO: the rank's own arrays stand in for its neighbours'
   bool stand_in() const { return mode_ == SOLO || (mode_ == RCCL && self_); }
   // RCCL peer of neighbour rank q (RCCL-SOLO: every peer is this process's only rank)
@@ -265,6 +290,7 @@ class Comm {
                        size_t esz, bool is_double, hipStream_t s) {
     char* base = (char*)a;
     const size_t pb = (size_t)plane * esz;
+    settle(s);
     if (mode_ == RCCL && self_) {  // SOLO's bytes: own boundary planes into own ghost planes
       std::vector<SelfPair> q;
       if (has_lo) q.push_back({base - depth * pb, base, depth * pb});
@@ -331,6 +357,7 @@ class Comm {
     char* recv_hi = base + (size_t)(nz + D) * pb;
     char* send_up = base + (ptrdiff_t)(nz - D - d) * (ptrdiff_t)pb;
     char* recv_lo = base - (ptrdiff_t)(D + d) * (ptrdiff_t)pb;
+    settle(s);
     if (mode_ == RCCL && self_) {  // SOLO's bytes
       std::vector<SelfPair> q;
       if (has_lo) q.push_back({recv_lo, send_up, d * pb});
@@ -382,6 +409,7 @@ class Comm {
   // counts are multiples of 4 (fp32 / fp64 volumes).
   void exchange_blocks(const std::vector<const void*>& send, const std::vector<size_t>& sbytes,
                        const std::vector<void*>& recv, const std::vector<size_t>& rbytes, hipStream_t s) {
+    settle(s);
     if (mode_ == RCCL && self_) {  // the own blocks stand in for the peers' (as SOLO)
       std::vector<SelfPair> q;
       for (int r = 0; r < nranks_; ++r)
@@ -420,6 +448,7 @@ class Comm {
   }
 
   void allreduce_sum_f64(double* p, size_t n, hipStream_t s) {
+    settle(s);
     if (mode_ == RCCL) {
       NCCL_CHECK(ncclAllReduce(p, p, n, ncclDouble, ncclSum, comm_, s));
       return;
@@ -441,6 +470,7 @@ class Comm {
   // host-side reduction of n doubles over the ranks (op 0 sum, 1 max), through a device
   // buffer on stream s: the bench's barrier and max-over-ranks timing without torch
   void allreduce_host(double* v, size_t n, int op, hipStream_t s) {
+    settle(s);
     if (mode_ == RCCL) {
       double* d = nullptr;
       HIPC_CHECK(hipMalloc(&d, sizeof(double) * n));
@@ -484,6 +514,7 @@ class Comm {
       return;
     }
     if (mode_ != RCCL) return;
+    settle(s);
     hipIpcMemHandle_t mine;
     HIPC_CHECK(hipIpcGetMemHandle(&mine, base));
     const size_t hb = sizeof(hipIpcMemHandle_t);
@@ -521,6 +552,7 @@ class Comm {
 
   // logical AND of one flag over the ranks (collective)
   bool all_true(bool v, hipStream_t s) {
+    settle(s);
     if (mode_ == RCCL && !self_) {
       int32_t* d = nullptr;
       int32_t h = v ? 1 : 0;
@@ -557,6 +589,7 @@ class Comm {
   void allgather_slabs(const void* slab, void* full, int64_t plane, int64_t nz_global, size_t esz,
                        hipStream_t s) {
     const size_t bytes = (size_t)plane * (size_t)(nz_global / nranks_) * esz;
+    settle(s);
     if (mode_ == RCCL && self_) {  // the own slab into every rank's slot (as SOLO)
       std::vector<SelfPair> q;
       for (int r = 0; r < nranks_; ++r) q.push_back({(char*)full + r * bytes, slab, bytes});
@@ -590,6 +623,8 @@ class Comm {
   int nranks_ = 1;
   int rank_ = 0;
   bool self_ = false;
+  bool graph_pending_ = false;        // a graph with RCCL operations may still be running
+  hipStream_t graph_stream_ = nullptr;
 };
 
 }  // namespace mad

@@ -1499,6 +1499,7 @@ class Solver final : public SolverBase {
       for (auto& L : lv_) vgraph_ptrs_.emplace_back(L.x, L.t);
     }
     HIP_CHECK(hipGraphLaunch(vgraph_, c_->stream));
+    if (ranks) c_->comm.graph_launched(c_->stream);
     if (ranks) {
       for (size_t l = 0; l < lv_.size(); ++l) {
         lv_[l].x_halo_ok = vgraph_exit_flags_[l].x_ok;

@@ -1,7 +1,9 @@
+# two RCCL ranks sharing one GPU: V-cycle forms (tools/rehearse_vcycles.py) and the bench's N = 2 launch
 set -o pipefail
-tr() { port=$1; shift; echo "== $*"; timeout -k 10 60 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port tools/rehearse_vcycles.py "$@" 2>&1 | grep -E "^\[rank|WARN|Error" ; echo "rc=$?"; }
+tr() { port=$1; shift; echo "== $*"; timeout -k 10 60 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port tools/rehearse_vcycles.py "$@" 2>&1 | grep -E "^\[rank|WARN|Error"; echo "rc=$?"; }
 tr 29621 --sync
 tr 29622
-tr 29623 --eager
+MAD_HIP_LIB=tools/pglibs/libmad_nosettle.so tr 29623
 tr 29624 --options 4
-tr 29625 --size 256
+echo "== bench rehearsal rccl"
+MAD_BENCH_SHARED_GPU=1 timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29625 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --no-precision-cycles --halo rccl 2>&1 | grep -E "bench rank|metric|WARN|Error"; echo "rc=$?"
