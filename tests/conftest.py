@@ -69,7 +69,10 @@ def pytest_sessionstart(session):
         # rank makes them two hosts to RCCL, so they connect over its socket transport
         # (loopback) -- real two-process RCCL (bootstrap, grouped send/recv, allreduce,
         # allgather, graph-captured V-cycles), with host-staged bytes instead of xGMI.
-        world, shared = 2, True
+        # (MAD_SHARED_MULTIPROC_WORLD: more rank processes on the one GPU, e.g. 4 for interior
+        # ranks with two neighbours; each one polls its neighbours' peer counters with <= 128
+        # workgroups, so a few ranks leave the sweeps they wait for enough CUs)
+        world, shared = max(2, min(4, int(os.environ.get("MAD_SHARED_MULTIPROC_WORLD", "2")))), True
     outdir = tempfile.mkdtemp(prefix="mad_mp_")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                WORLD_SIZE=str(world))
