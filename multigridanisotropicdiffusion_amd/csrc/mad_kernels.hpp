@@ -1682,7 +1682,16 @@ __global__ void __launch_bounds__(256) brec_scatter_k(const T* __restrict__ b, T
 }
 
 // ---------------------------------------------------------------------------
-// coarsest-grid solve x = A^-1 b with the precomputed fp64 inverse: one wave per row
+// coarsest-grid solve x = A^-1 b with the precomputed fp64 inverse: one wave per row.  The row
+// dot product is one function (default fp contraction) shared with vtail_k, so both round alike.
+template <typename T>
+__device__ __forceinline__ double coarse_row_dot(const double* __restrict__ a, const T* __restrict__ b,
+                                                 int n, int lane) {
+  double s = 0.0;
+  for (int c = lane; c < n; c += 64) s += a[c] * (double)b[c];
+  return wave_sum(s);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) coarse_solve_k(const double* __restrict__ inv,
                                                       const T* __restrict__ b, T* __restrict__ x,
@@ -1690,10 +1699,7 @@ __global__ void __launch_bounds__(256) coarse_solve_k(const double* __restrict__
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n) return;
-  const double* a = inv + (int64_t)row * n;
-  double s = 0.0;
-  for (int c = lane; c < n; c += 64) s += a[c] * (double)b[c];
-  s = wave_sum(s);
+  const double s = coarse_row_dot(inv + (int64_t)row * n, b, n, lane);
   if (lane == 0) x[row] = (T)s;
 }
 
@@ -1810,10 +1816,7 @@ __global__ void __launch_bounds__(1024) vtail_k(TailArgs<T> a) {
     const int n = (int)C.g.N;
     const int lane = tid & 63;
     for (int row = tid >> 6; row < n; row += nt >> 6) {
-      const double* ar = a.inv + (int64_t)row * n;
-      double sacc = 0.0;
-      for (int c = lane; c < n; c += 64) sacc += ar[c] * (double)C.b[c];
-      sacc = wave_sum(sacc);
+      const double sacc = coarse_row_dot(a.inv + (int64_t)row * n, (const T*)C.b, n, lane);
       if (lane == 0) C.x[row] = (T)sacc;
     }
     __syncthreads();
