@@ -435,8 +435,14 @@ struct PeerOut {
   uint32_t* sig[2];
 };
 
+//
+// BL (dense b, not BREC): b is staged through LDS like u -- one coalesced load of the tile region's
+// plane per step into a ring of NC planes (the stages read plane k - c at step k), the stages then
+// read their point's b from LDS at the u offset -- instead of one load per stage point of its colour,
+// which on the x-parity-interleaved dense b is a stride-2 access (two cache lines per wave load for
+// one line's worth of values).  The LDS then holds NP + NC planes (fp32 64 x 32 tiles: 155 KB).
 template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false,
-          bool PEER = false>
+          bool PEER = false, bool BL = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
@@ -453,6 +459,8 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   constexpr uint32_t TS = sizeof(T);
   static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
   static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
+  static_assert(!(BL && BREC), "b rides in the record");
+  constexpr int NB = BL ? NC : 0;  // b ring slots (after the NP u slots)
   extern __shared__ __align__(16) unsigned char fused_smem[];
 
   int bid = blockIdx.x;
@@ -613,8 +621,27 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   unsigned char* lbytes = fused_smem;
 
   T up[UPT];
+  T bp[BL ? UPT : 1];
   T raw[NC][RS];
   T bv[NC];
+  auto bslot = [](int m) { return NP + (m + NB * 64) % (NB > 0 ? NB : 1); };
+  auto load_bplane = [&](int m) {
+    if constexpr (BL) {
+      m = min(max(m, zlo), zhi - 1);
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(b + (int64_t)m * sz);
+#pragma unroll
+      for (int e = 0; e < UPT; ++e) bp[e] = buf_load<T>(rs, usrc[e], 0u);
+    }
+  };
+  auto put_bplane = [&](int m) {
+    if constexpr (BL) {
+      unsigned char* P = lbytes + bslot(m) * (PLANE * TS);
+#pragma unroll
+      for (int e = 0; e < UPT; ++e) {
+        if (e < UPT - 1 || udst[e] >= 0) *reinterpret_cast<T*>(P + udst[e]) = bp[e];
+      }
+    }
+  };
   auto load_plane = [&](int m) {
     m = min(max(m, zlo), zhi - 1);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
@@ -637,7 +664,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       const PD d = pdelta(c, PM);
       buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * RS), pg[c][PM % NPM],
                           raw[c]);
-      if constexpr (!BREC)
+      if constexpr (!BREC && !BL)
         bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
     }
   };
@@ -686,7 +713,14 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     coefs_from_raw<T, 3, KIND>(raw[c], rat, q);
     T D, S;
     stencil_combine<T, 3, KIND>(q, nb, D, S);
-    const T v = gs_update(BREC ? raw[c][NCF] : bv[c], S, D);
+    T bval;
+    if constexpr (BREC)
+      bval = raw[c][NCF];
+    else if constexpr (BL)
+      bval = *reinterpret_cast<const T*>(lbytes + bslot(m) * (PLANE * TS) + o);
+    else
+      bval = bv[c];
+    const T v = gs_update(bval, S, D);
     const int bit = c * 2 + PM;
     if (interior) {
       if (NC == 2 || FG::rows(c) * FG::cols(c) < NT) {
@@ -720,6 +754,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       put_plane(m);
     }
   load_plane(kbeg + 1);
+  load_bplane(kbeg);
 #pragma unroll
   for (int c = 0; c < LEAD; ++c) load_stage(c, kbeg, c & 1);
 
@@ -733,6 +768,8 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
         asm volatile("" : "+v"(vmask), "+v"(gmask), "+v"(omask));
         if (plane_ok(k + 1)) put_plane(k + 1);
         load_plane(k + 2);
+        put_bplane(k);  // b of plane k: stage c reads plane k - c at step k (ring of NC)
+        load_bplane(k + 1);
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < NC; ++c) {

@@ -712,9 +712,14 @@ class Solver final : public SolverBase {
     const unsigned nb = (unsigned)(tiles * zr.nchunks);
     constexpr int NC = (KD == KFULL) ? 4 : 2;
     using FG = FusedGeom<NC, TX, TY>;
-    constexpr size_t lds = sizeof(T) * FG::NP * FG::PLANE;
-    REQUIRE(lds <= 160 * 1024, MAD_ERR_UNSUPPORTED,
-            "fused GS tile needs " + std::to_string(lds) + " B of LDS (> 160 KiB)");
+    constexpr size_t lds_u = sizeof(T) * FG::NP * FG::PLANE;
+    REQUIRE(lds_u <= 160 * 1024, MAD_ERR_UNSUPPORTED,
+            "fused GS tile needs " + std::to_string(lds_u) + " B of LDS (> 160 KiB)");
+    // dense b staged through LDS where its ring fits beside the u ring (fp32; fp64 tiles do not)
+    constexpr size_t lds_bl = sizeof(T) * (FG::NP + NC) * FG::PLANE;
+    constexpr bool bl_fits = lds_bl <= 160 * 1024;
+    const bool bl = fused_b_lds(L);
+    const size_t lds = bl ? lds_bl : lds_u;
     // fp64 doubles the register footprint: 2 waves per SIMD (one 512-thread block per CU,
     // which is all its LDS allows anyway)
     constexpr int MW = sizeof(T) == 8 ? 2 : 4;
@@ -734,14 +739,27 @@ class Solver final : public SolverBase {
     if (part == 4) {
       if (L.brec)
         run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true, true>);
+      else if constexpr (bl_fits)
+        bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true, true>)
+           : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>);
       else
         run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>);
     } else if (L.brec) {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
+    } else if constexpr (bl_fits) {
+      bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true>)
+         : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
     } else {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
     }
   }
+
+  // does level L's fused sweep stage its dense b through LDS (gs_fused3_k BL)?  fp32 only: the
+  // fp64 tiles' u ring leaves no room for a b ring
+#ifndef MAD_FUSED_B_LDS
+#define MAD_FUSED_B_LDS 1
+#endif
+  bool fused_b_lds(const LevelData<T>& L) const { return MAD_FUSED_B_LDS && sizeof(T) == 4 && !L.brec; }
 
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
   void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {
@@ -787,9 +805,10 @@ class Solver final : public SolverBase {
       const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : 1024;
       const bool brec = lv_[l].brec;
       const LevelData<T>& L = lv_[l];
-      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER last)
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s>", tn, kind, tx, ty, nt,
-                    sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false", L.peer ? "true" : "false");
+      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER, BL last)
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s, %s>", tn, kind, tx, ty,
+                    nt, sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false", L.peer ? "true" : "false",
+                    fused_b_lds(L) ? "true" : "false");
       // rank slabs: which sweep form fused_sweep takes
       if (L.peer) return std::string(buf) + " [rank slab: peer halo, edge planes stored by the sweep]";
       if (sweep_overlap(l)) {
