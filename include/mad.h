@@ -166,11 +166,6 @@ typedef struct mad_desc {
    launch) -- no exchange after the sweep.  Levels whose sweeps are not fused single launches keep the
    exchange.  Identical results.  Setup-time option (mad_setup maps the windows, collectively). */
 #define MAD_OPT_PEER_HALO 4u
-/* MAD_OPT_NO_VCYCLE_TAIL: run every coarse level of a V-cycle with its own launches (per-colour GS
-   passes, descent, prolongation, coarsest solve) instead of the default single-workgroup tail kernel
-   for the replicated 3D levels of <= 32768 voxels and below (multicolour GS, dense coarsest inverse).
-   Identical results; the reference of the tail's parity test. */
-#define MAD_OPT_NO_VCYCLE_TAIL 8u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

@@ -1720,7 +1720,7 @@ __global__ void __launch_bounds__(256) brec_scatter_k(const T* __restrict__ b, T
 
 // ---------------------------------------------------------------------------
 // coarsest-grid solve x = A^-1 b with the precomputed fp64 inverse: one wave per row.  The row
-// dot product is one function (default fp contraction) shared with vtail_k, so both round alike.
+// dot product: default fp contraction (a kernel that inlines it keeps that, whatever its own pragmas).
 template <typename T>
 __device__ __forceinline__ double coarse_row_dot(const double* __restrict__ a, const T* __restrict__ b,
                                                  int n, int lane) {
@@ -1738,156 +1738,6 @@ __global__ void __launch_bounds__(256) coarse_solve_k(const double* __restrict__
   if (row >= n) return;
   const double s = coarse_row_dot(inv + (int64_t)row * n, b, n, lane);
   if (lane == 0) x[row] = (T)s;
-}
-
-// ---------------------------------------------------------------------------
-// V-cycle tail: the small coarse levels of a V-cycle -- from a level l0 down to the coarsest and
-// back (nu multicolour GS sweeps, residual, restriction with the coarse x zeroed, the coarsest
-// solve with the dense inverse, interpolation + add, nu sweeps) -- in ONE workgroup.  Every point
-// goes through the same device functions in the same order as the launches it replaces
-// (gs_color_k per colour, residual_k + restrict_k -- equal to resid_restrict3_k --, coarse_solve_k's
-// per-row wave reduction, interp_k -- equal to interp3_k --), so the result is bit-identical; on
-// these levels each of those ~19 launches per level costs ~5 us of dispatch for microseconds of
-// work, and here a phase costs one workgroup barrier.
-template <typename T>
-struct TailLevel {
-  T* x;
-  T* b;
-  T* r;
-  const T* cf;
-  Geo g;
-  Rat<T> rat;
-  int cent[3];
-};
-constexpr int TAIL_MAX_LEVELS = 6;
-template <typename T>
-struct TailArgs {
-  TailLevel<T> lv[TAIL_MAX_LEVELS];
-  int nlev;           // levels in lv; the last one is the coarsest (dense inverse)
-  int nu;             // sweeps before and after the coarse-grid correction
-  int ncolors;        // 4 (19-point) or 2 (7-point)
-  const double* inv;  // coarsest inverse, row-major n x n
-};
-
-template <typename T, int KIND>
-__global__ void __launch_bounds__(1024) vtail_k(TailArgs<T> a) {
-#pragma clang fp contract(off)  // the transfer formulas' explicit fma (as restrict_k / interp_k)
-  const int tid = threadIdx.x;
-  const int nt = blockDim.x;
-  auto sweeps = [&](const TailLevel<T>& L) {
-    const Geo& g = L.g;
-    const int hx = (g.nx + 1) / 2;
-    const int rows = (a.ncolors == 4) ? (g.ny + 1) / 2 : g.ny;
-    const int cnt = hx * rows * g.nz;
-    for (int sw = 0; sw < a.nu; ++sw)
-      for (int color = 0; color < a.ncolors; ++color) {
-        for (int q = tid; q < cnt; q += nt) {
-          const int iq = q % hx;
-          const int t = q / hx;
-          const int jq = t % rows;
-          const int k = t / rows;
-          const int kg = k + g.zoff;
-          int i, j;
-          if (a.ncolors == 4) {
-            j = 2 * jq + (((color >> 1) ^ kg) & 1);
-            i = 2 * iq + (((color & 1) ^ kg) & 1);
-          } else {
-            j = jq;
-            i = 2 * iq + ((color + j + kg) & 1);
-          }
-          if (i >= g.nx || j >= g.ny) continue;
-          const int64_t p = i + g.sy * j + g.sz * k;
-          T D, S;
-          stencil_terms<T, 3, KIND>(L.x, L.cf, g, L.rat, i, j, k, p, D, S);
-          L.x[p] = gs_update(L.b[p], S, D);
-        }
-        __syncthreads();
-      }
-  };
-  // descent
-  for (int d = 0; d + 1 < a.nlev; ++d) {
-    const TailLevel<T>& F = a.lv[d];
-    const TailLevel<T>& C = a.lv[d + 1];
-    sweeps(F);
-    const Geo& g = F.g;
-    for (int q = tid; q < (int)g.N; q += nt) {
-      const int i = q % g.nx, t = q / g.nx, j = t % g.ny, k = t / g.ny;
-      const int64_t p = i + g.sy * j + g.sz * k;
-      T D, S;
-      stencil_terms<T, 3, KIND>(F.x, F.cf, g, F.rat, i, j, k, p, D, S);
-      F.r[p] = resid_value(F.b[p], D, F.x[p], S);
-    }
-    __syncthreads();
-    const Geo& gc = C.g;
-    for (int q = tid; q < (int)gc.N; q += nt) {
-      const int I = q % gc.nx, t = q / gc.nx, J = t % gc.ny, K = t / gc.ny;
-      int ix[4], iy[4], iz[4];
-      T wx[4], wy[4], wz[4];
-      rtaps4<T>(I, gc.nx, C.cent[0], ix, wx);
-      rtaps4<T>(J, gc.ny, C.cent[1], iy, wy);
-      rtaps4<T>(K, gc.nz, C.cent[2], iz, wz);
-      T v = T(0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const T* pl = F.r + g.sz * (int64_t)iz[c];
-        T vz = T(0);
-#pragma unroll
-        for (int bq = 0; bq < 4; ++bq) {
-          const T* row = pl + g.sy * iy[bq];
-          T vy = T(0);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) vy = fma(wx[e], row[ix[e]], vy);
-          vz = fma(wy[bq], vy, vz);
-        }
-        v = fma(wz[c], vz, v);
-      }
-      const int64_t pc = I + gc.sy * J + gc.sz * K;
-      C.b[pc] = v;
-      C.x[pc] = T(0);
-    }
-    __syncthreads();
-  }
-  // coarsest: x = A^-1 b, one wave per row (coarse_solve_k's reduction)
-  {
-    const TailLevel<T>& C = a.lv[a.nlev - 1];
-    const int n = (int)C.g.N;
-    const int lane = tid & 63;
-    for (int row = tid >> 6; row < n; row += nt >> 6) {
-      const double sacc = coarse_row_dot(a.inv + (int64_t)row * n, (const T*)C.b, n, lane);
-      if (lane == 0) C.x[row] = (T)sacc;
-    }
-    __syncthreads();
-  }
-  // ascent
-  for (int d = a.nlev - 2; d >= 0; --d) {
-    const TailLevel<T>& F = a.lv[d];
-    const TailLevel<T>& C = a.lv[d + 1];
-    const Geo& g = F.g;
-    const Geo& gc = C.g;
-    for (int q = tid; q < (int)g.N; q += nt) {
-      const int i = q % g.nx, t = q / g.nx, j = t % g.ny, k = t / g.ny;
-      int ix[2], iy[2], iz[2];
-      T wx[2], wy[2], wz[2];
-      itaps2<T>(i, gc.nx, C.cent[0], ix, wx);
-      itaps2<T>(j, gc.ny, C.cent[1], iy, wy);
-      itaps2<T>(k, gc.nz, C.cent[2], iz, wz);
-      T v = T(0);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const T* pl = C.x + gc.sz * (int64_t)iz[c];
-        T vz = T(0);
-#pragma unroll
-        for (int bq = 0; bq < 2; ++bq) {
-          const T* row = pl + gc.sy * iy[bq];
-          vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
-        }
-        v = fma(wz[c], vz, v);
-      }
-      F.x[i + g.sy * j + g.sz * k] += v;
-    }
-    __syncthreads();
-    sweeps(F);
-  }
 }
 
 // ---------------------------------------------------------------------------

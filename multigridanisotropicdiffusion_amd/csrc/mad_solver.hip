@@ -1297,59 +1297,11 @@ class Solver final : public SolverBase {
   }
 
   // ------------------------------------------------------------- cycles
-  // ------------------------------------------------------------- V-cycle tail
-  // Levels at or below this many voxels (and everything coarser) run as one vtail_k workgroup
-  // instead of ~19 launches per level (multicolour GS, 3D, replicated, dense coarsest inverse).
-#ifndef MAD_TAIL_MAX_VOXELS
-#define MAD_TAIL_MAX_VOXELS 32768
-#endif
-  static constexpr int64_t TAIL_MAX_VOXELS = MAD_TAIL_MAX_VOXELS;
-  bool tail_ok(int l) const {
-    const int nl = c_->nlev;
-    if (c_->dim != 3 || c_->d.smoother != MAD_GAUSS_SEIDEL || c_->d.verbose) return false;
-    if (c_->d.options & MAD_OPT_NO_VCYCLE_TAIL) return false;
-    if (nl - l < 2 || nl - l > TAIL_MAX_LEVELS || cblk_.active() || !inv_) return false;
-    if (lv_[l].g.N > TAIL_MAX_VOXELS) return false;
-    for (int q = l; q < nl; ++q)
-      if (c_->geom[q].distributed || lv_[q].brec || (q < nl - 1 && use_fused(q))) return false;
-    return true;
-  }
-  void launch_tail(int l) {
-    const int nl = c_->nlev;
-    TailArgs<T> a{};
-    a.nlev = nl - l;
-    a.nu = (int)c_->d.iterations_per_grid;
-    a.ncolors = c_->ncolors;
-    a.inv = inv_;
-    for (int q = l; q < nl; ++q) {
-      LevelData<T>& L = lv_[q];
-      TailLevel<T>& t = a.lv[q - l];
-      t.x = L.x;
-      t.b = L.b;
-      t.r = L.r;
-      t.cf = L.cf;
-      t.g = L.g;
-      t.rat = L.rat;
-      for (int d = 0; d < 3; ++d) t.cent[d] = L.cent[d];
-      L.b_halo_ok = L.brec_ok = false;
-      x_changed(q);
-    }
-    dispatch(3, c_->kind, [&](auto D, auto K) {
-      (void)D;
-      hipLaunchKernelGGL((vtail_k<T, K.value>), dim3(1), dim3(1024), 0, c_->stream, a);
-    });
-    HIP_CHECK(hipGetLastError());
-  }
-
   void vcycle_rec(int l) {
     const int nl = c_->nlev;
     if (l == nl - 1) {  // MAD.hxx:356-371
       coarse_solve();
       if (c_->d.verbose) verbose_line(l, -1, "direct solver");
-      return;
-    }
-    if (tail_ok(l)) {  // this level and all coarser ones in one workgroup
-      launch_tail(l);
       return;
     }
     const unsigned nu = c_->d.iterations_per_grid;
@@ -2566,8 +2518,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             "bad rank / nranks");
     REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
-    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO |
-                            MAD_OPT_NO_VCYCLE_TAIL)) == 0,
+    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO)) == 0,
             MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
