@@ -759,7 +759,11 @@ class Solver final : public SolverBase {
 #ifndef MAD_FUSED_B_LDS
 #define MAD_FUSED_B_LDS 1
 #endif
-  bool fused_b_lds(const LevelData<T>& L) const { return MAD_FUSED_B_LDS && sizeof(T) == 4 && !L.brec; }
+  // (level 0 only: 1249.7 vs 1279.6 us per 512^3 launch, but 195.7 vs 190.8 us at 256^3,
+  // profiles/r04_bl_ab.md)
+  bool fused_b_lds(const LevelData<T>& L) const {
+    return MAD_FUSED_B_LDS && sizeof(T) == 4 && !L.brec && &L == &lv_[0];
+  }
 
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
   void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {

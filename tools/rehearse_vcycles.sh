@@ -3,7 +3,6 @@ set -o pipefail
 tr() { port=$1; shift; echo "== $*"; timeout -k 10 60 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port tools/rehearse_vcycles.py "$@" 2>&1 | grep -E "^\[rank|WARN|Error"; echo "rc=$?"; }
 tr 29621 --sync
 tr 29622
-MAD_HIP_LIB=tools/pglibs/libmad_nosettle.so tr 29623
 tr 29624 --options 4
 echo "== bench rehearsal rccl"
 MAD_BENCH_SHARED_GPU=1 timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29625 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --no-precision-cycles --halo rccl 2>&1 | grep -E "bench rank|metric|WARN|Error"; echo "rc=$?"
