@@ -28,6 +28,10 @@ def drive(s, M):
     for q in range(VCYCLES):
         s.vcycle()
         out[f"vcycle{q + 1}"] = s.download(0, M.capi.X).astype(np.float32)
+    # graph replays back to back (no host synchronisation between them), as bench.py runs them:
+    # each replay's eager entry work must not overtake the previous replay's RCCL operations
+    s.bench_vcycle(3)
+    out["vcycles_back_to_back"] = s.download(0, M.capi.X).astype(np.float32)
     return out
 
 
