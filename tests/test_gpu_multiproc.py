@@ -5,7 +5,8 @@ start, before this process touches a GPU, when the gpu tests are selected; here 
 and their rank slabs compared BIT for bit with the same sequence on the in-process LOCAL
 transport (ranks as threads on one device; itself bitwise equal to the single-rank run,
 test_gpu_distributed_full.py): two level-0 sweeps and three V-cycles at 512^3, the later ones
-replaying the captured multi-rank hipGraph over RCCL -- once with the default exchange (grouped
+replaying the captured multi-rank hipGraph over RCCL, then three replays back to back (no host
+synchronisation between them, as bench.py runs them) -- once with the default exchange (grouped
 ncclSend / ncclRecv after each sweep) and once with MAD_OPT_PEER_HALO (the sweep stores its edge
 planes into the neighbours' mailboxes, mapped across the processes with hipIpc handles).
 
