@@ -38,7 +38,8 @@ def _multi(nranks, fn, T, **kw):
 @pytest.mark.parametrize("smoother,gs_kernel,cycle,options", [(0, 0, 0, 0), (0, 1, 0, 0), (2, 0, 0, 0),
                                                               (0, 3, 0, 0), (0, 3, 2, 0), (0, 3, 0, 2),
                                                               (0, 3, 2, 2), (0, 3, 0, 4), (0, 3, 2, 4)])
-def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle, options):
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle, options, precision):
     """cycle 2 (SMOOTHER): level-0 records carry b (sync_brec on ghost planes).  gs_kernel 3 forces
     the fused sweep on these small levels, in its default serial rank form (one launch, then the
     exchange) or with options 2 (MAD_OPT_OVERLAP_RANK_SWEEP) in the split form (boundary chunks,
@@ -61,7 +62,8 @@ def test_sweeps_and_vcycles_bitwise(nranks, smoother, gs_kernel, cycle, options)
         s.vcycle()
         v = s.download(0, M.capi.X)
         return a, v, s.residual(0)
-    kw = dict(smoother=smoother, gs_kernel=gs_kernel, cycle=cycle, options=options)
+    kw = dict(smoother=smoother, gs_kernel=gs_kernel, cycle=cycle, options=options,
+              precision=M.FP32 if precision == "fp32" else M.FP64)
     ref = _single(fn, T, **kw)
     out = _multi(nranks, fn, T, **kw)
     np.testing.assert_array_equal(np.concatenate([o[0] for o in out]), ref[0])
@@ -115,6 +117,19 @@ def test_slab_tensor_setup_is_bitwise(nranks):
 @pytest.mark.parametrize("nranks", [2, 4])
 def test_distributed_filter_run_matches_single(nranks):
     """mad_run on slabs (each rank passes its own slab of the image)."""
+    _filter_run(nranks)
+
+
+@pytest.mark.parametrize("tolerance", [1e-6, 1e-10])
+def test_distributed_filter_run_with_peer_halo(tolerance):
+    """mad_run with MAD_OPT_PEER_HALO and the fused sweep forced (gs_kernel 3) on 2-rank slabs: the
+    peer batches are taken in at every ghost-plane use (norms, descents, interpolations, the next
+    time step's casts); at 1e-10 the default precision is FP32_REFINE (fp64 residual, fp32 cycles)."""
+    import multigridanisotropicdiffusion_amd as M
+    _filter_run(2, tolerance=tolerance, options=M.capi.OPT_PEER_HALO, gs_kernel=3, number_of_steps=2)
+
+
+def _filter_run(nranks, tolerance=1e-6, **kw):
     from multigridanisotropicdiffusion_amd import distributed as D
     T = synth.ved_form(SHAPE)
     img = (synth.image(SHAPE, seed=5) * 100).astype(np.float32)
@@ -124,8 +139,8 @@ def test_distributed_filter_run_matches_single(nranks):
         z0, z1 = (0, SHAPE[0]) if r is None else sl[r]
         out, st = s.run(img[z0:z1], out_dtype=np.float32)
         return out, st
-    ref, rst = _single(fn, T, tolerance=1e-6)
-    outs = _multi(nranks, fn, T, tolerance=1e-6)
+    ref, rst = _single(fn, T, tolerance=tolerance, **kw)
+    outs = _multi(nranks, fn, T, tolerance=tolerance, **kw)
     full = np.concatenate([o[0] for o in outs])
     assert np.abs(full - ref).max() <= 1e-5 * np.abs(ref).max()
     assert all(o[1]["total_cycles"] == rst["total_cycles"] for o in outs)
