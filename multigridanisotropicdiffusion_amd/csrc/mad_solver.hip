@@ -244,6 +244,8 @@ struct SolverBase {
   virtual bool residual_restrict(int l) = 0;  // fused b[l+1] <- R (b - A x); false: not applicable
   virtual void interpolate(int l, bool add) = 0;
   virtual void coarse_solve() = 0;
+  // errors the device reported asynchronously (a peer-halo wait that timed out)
+  virtual void check_device_errors() {}
   virtual void vcycle() = 0;
   virtual void fmg() = 0;
   virtual void run(const void* in, int in_dtype, void* out, int out_dtype, bool dev_io,
@@ -535,6 +537,7 @@ class Solver final : public SolverBase {
   void peer_resolve_all() {
     for (size_t l = 0; l < lv_.size(); ++l) peer_resolve((int)l);
   }
+  void check_device_errors() override { peer_check(); }
   // a peer wait that timed out (a neighbour never delivered) is an error, not silent stale halos
   void peer_check() {
     for (auto& L : lv_) {
@@ -542,7 +545,7 @@ class Solver final : public SolverBase {
       uint32_t err = 0;
       HIP_CHECK(hipMemcpyAsync(&err, peer_ctl(L.win, L) + 5, sizeof err, hipMemcpyDeviceToHost, c_->stream));
       HIP_CHECK(hipStreamSynchronize(c_->stream));
-      if (err) throw std::runtime_error("peer halo: a neighbour's edge planes never arrived (wait timed out)");
+      if (err) throw CommError("peer halo: a neighbour's edge planes never arrived (wait timed out)");
     }
   }
 
@@ -2881,6 +2884,7 @@ int mad_synchronize(mad_ctx* c) {
     use_device(c);
     HIP_CHECK(hipStreamSynchronize(c->stream));
     HIP_CHECK(hipStreamSynchronize(c->comm_stream));
+    if (c->solver) c->solver->check_device_errors();
   });
 }
 
