@@ -822,6 +822,51 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   }
 }
 
+// Peer halo self-test at setup (Solver::peer_selftest): each edge writes a token into the
+// neighbour's mailbox with the sweep's store / completion / counter pattern (peer_ping_k), then
+// every rank checks that both neighbours' tokens and counts arrived (peer_pong_k, bounded wait),
+// resets its counters and reports -- so a cross-GPU path that does not deliver is found before
+// the first sweep, and the ranks fall back to the exchange together.
+template <typename T>
+__global__ void __launch_bounds__(64) peer_ping_k(PeerOut<T> po, T token) {
+  T* d = po.dst[blockIdx.x];
+  if (!d) return;
+  d[threadIdx.x] = token;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(po.sig[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) peer_pong_k(const T* mlo, const T* mhi, uint32_t* clo, uint32_t* chi,
+                                                  T tlo, T thi, uint32_t* okw, uint64_t tmo) {
+  __shared__ int good;
+  if (threadIdx.x == 0) {
+    good = 1;
+    uint32_t* cs[2] = {clo, chi};
+    for (int q = 0; q < 2; ++q) {
+      if (!cs[q]) continue;
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(cs[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < 1u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > tmo) {
+          good = 0;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const bool bad = (mlo && mlo[threadIdx.x] != tlo) || (mhi && mhi[threadIdx.x] != thi);
+  if (bad) atomicAnd(&good, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (clo) __hip_atomic_store(clo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (chi) __hip_atomic_store(chi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(okw, (uint32_t)good, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Peer halo, consumer side: wait for the neighbours' edge planes, copy the two mailboxes into
 // the ghost planes.  blockIdx.y = side (0: from rank - 1 into the lower ghost planes, 1: from
 // rank + 1 into the upper ones; a null destination = no neighbour there).  ctl is this rank's

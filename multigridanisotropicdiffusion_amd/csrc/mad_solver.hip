@@ -485,11 +485,46 @@ class Solver final : public SolverBase {
         L.win = nullptr;
         continue;
       }
+      if (!peer_selftest(L)) {
+        // a neighbour's token or count did not arrive on some rank: every rank exchanges instead
+        Comm::close_window(L.win_lo, L.win_ipc);
+        Comm::close_window(L.win_hi, L.win_ipc);
+        L.win_lo = L.win_hi = nullptr;
+        HIP_CHECK(hipFree(L.win));
+        L.win = nullptr;
+        peer_fallbacks_ += 1;
+        continue;
+      }
       int tiles = 0, nchunks = 0;
       fused_shape(L, &tiles, &nchunks);
       L.peer_tiles = (uint32_t)tiles;
       L.peer = true;
     }
+  }
+  // one token per edge through the mapped windows, checked on every rank (collective)
+  bool peer_selftest(LevelData<T>& L) {
+    const int r = c_->comm.rank();
+    const bool self = c_->comm.stand_in();
+    auto token = [](int rank) { return T(1000) * T(rank + 1) + T(7); };
+    hipLaunchKernelGGL((peer_ping_k<T>), dim3(2), dim3(64), 0, c_->stream, peer_out(L, 0), token(r));
+    HIP_CHECK(hipGetLastError());
+    // the in-process transport's ranks share one device's hardware queues: all pings done first
+    c_->comm.local_barrier(c_->stream);
+    const int64_t top = (int64_t)(GHOST - 1) * L.g.sz;
+    const T* mlo = nullptr;
+    const T* mhi = nullptr;
+    if (L.g.zlo_ghost) mlo = mailbox(L.win, L, 0, 0) + (self ? 0 : top);
+    if (L.g.zhi_ghost) mhi = mailbox(L.win, L, 0, 1) + (self ? top : 0);
+    uint32_t* ctl = peer_ctl(L.win, L);
+    const uint64_t tmo = peer_timeout_ticks_ / 10;  // 2 s
+    hipLaunchKernelGGL((peer_pong_k<T>), dim3(1), dim3(64), 0, c_->stream, mlo, mhi,
+                       L.g.zlo_ghost ? ctl + 0 : nullptr, L.g.zhi_ghost ? ctl + 1 : nullptr,
+                       token(self ? r : r - 1), token(self ? r : r + 1), ctl + 6, tmo);
+    HIP_CHECK(hipGetLastError());
+    uint32_t ok = 0;
+    HIP_CHECK(hipMemcpyAsync(&ok, ctl + 6, sizeof ok, hipMemcpyDeviceToHost, c_->stream));
+    HIP_CHECK(hipStreamSynchronize(c_->stream));
+    return c_->comm.all_true(ok == 1u, c_->stream);
   }
   // where this rank's sweep into buffer `buf` stores its edge planes: the bottom edge chunk into
   // rank - 1's mailbox of planes above it (side 1), the top chunk (reflected: plane stride -sz) into
@@ -1916,6 +1951,7 @@ class Solver final : public SolverBase {
   std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
   bool vgraph_failed_ = false;
   uint64_t peer_timeout_ticks_ = 0;
+  int peer_fallbacks_ = 0;  // levels whose peer self-test failed (they exchange instead)
   std::vector<HaloFlags> vgraph_exit_flags_;  // rank slabs: ghost bookkeeping after one cycle
   int vcycles_eager_ = 0;  // rank slabs: cycles run eagerly so far (RCCL peers connected)
   int ncoef_ = 0;
