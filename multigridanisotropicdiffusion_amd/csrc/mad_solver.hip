@@ -1969,6 +1969,18 @@ class Solver final : public SolverBase {
 
   void release() {
     if (c_ && c_->comm_stream) (void)hipStreamSynchronize(c_->comm_stream);
+    // a neighbour's last peer batch still in flight lands in this rank's window: take it in (the
+    // unpack waits until the neighbour's stores are complete) before the window is freed.  The
+    // in-process transport's ranks drain their streams at their next barrier instead (no wait here:
+    // a barrier in a destructor could hang on a rank that already failed).
+    if (c_ && c_->comm.mode() != Comm::LOCAL) {
+      try {
+        for (size_t l = 0; l < lv_.size(); ++l)
+          if (lv_[l].x_peer_pending) peer_resolve((int)l);
+      } catch (...) {
+      }
+    }
+    if (c_ && c_->stream) (void)hipStreamSynchronize(c_->stream);
     if (vgraph_) (void)hipGraphExecDestroy(vgraph_);
     vgraph_ = nullptr;
     vgraph_ptrs_.clear();
