@@ -515,8 +515,12 @@ class Comm {
     }
     if (mode_ != RCCL) return;
     settle(s);
+    // a handle this rank cannot export still takes part in the gather (zeros) and votes no below,
+    // so no rank is left waiting in a collective the others skipped
     hipIpcMemHandle_t mine;
-    HIPC_CHECK(hipIpcGetMemHandle(&mine, base));
+    std::memset(&mine, 0, sizeof mine);
+    bool ok = hipIpcGetMemHandle(&mine, base) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
     const size_t hb = sizeof(hipIpcMemHandle_t);
     std::vector<char> all(hb * nranks_);
     char* d = nullptr;
@@ -529,7 +533,6 @@ class Comm {
     // a neighbour's window this process cannot map (no peer access between the two GPUs) makes
     // every rank give the windows up together -- the caller falls back to the exchange -- instead
     // of one rank throwing while the others wait in their next collective
-    bool ok = true;
     auto open = [&](int r, void** p) {
       hipIpcMemHandle_t h;
       std::memcpy(&h, all.data() + hb * r, hb);
@@ -539,8 +542,8 @@ class Comm {
         ok = false;
       }
     };
-    if (rank_ > 0) open(rank_ - 1, lo);
-    if (rank_ < nranks_ - 1) open(rank_ + 1, hi);
+    if (ok && rank_ > 0) open(rank_ - 1, lo);
+    if (ok && rank_ < nranks_ - 1) open(rank_ + 1, hi);
     *ipc = true;
     if (!all_true(ok, s)) {
       close_window(*lo, true);
