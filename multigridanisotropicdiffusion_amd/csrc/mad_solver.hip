@@ -1450,7 +1450,13 @@ class Solver final : public SolverBase {
   // ghost planes made current on the stream)
   void ranks_graph_entry() {
     peer_resolve_all();
-    halo(0, lv_[0].x, GHOST);
+    // level 0's x ghost planes: a peer level has them (resolved above); otherwise the graph exchanges
+    // them itself (its first sweep), so no eager RCCL call sits between two replays -- such a call
+    // must first wait for the previous replay (Comm::settle), which would stall the pipeline
+    if (lv_[0].peer)
+      halo(0, lv_[0].x, GHOST);
+    else
+      lv_[0].x_halo_ok = false;
     if (!lv_[0].brec && !lv_[0].b_halo_ok) {
       halo(0, lv_[0].b, GHOST);
       lv_[0].b_halo_ok = true;
