@@ -989,14 +989,19 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
 // One barrier per plane.  Needs the GHOST x/b planes and coefficient padding planes
 // of LevelData (masked lanes read inside them).  be / xe (MAD_FP32_REFINE's defect
 // correction): also be = (TE) r and xe = 0 at every point, the fp32 hierarchy's next rhs and
-// zero initial guess (convert_k + fill_k of r folded into this pass).
+// zero initial guess (convert_k + fill_k of r folded into this pass).  ue / uo (the defect
+// correction's update folded in, one GPU): every loaded u is u + (T) ue -- the fp32 cycle's
+// correction -- and the owned points' u + ue go to uo (a second buffer: neighbouring tiles still
+// read u); xe is then written by a separate fill, since those tiles also read ue.
 template <typename T, int KIND, int TX, int TY, bool BREC = false, typename TE = T>
 __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const T* __restrict__ b,
                                                     T* __restrict__ r, const T* __restrict__ cf,
                                                     Geo g, Rat<T> rat, int zc, int ntx,
                                                     double* __restrict__ part,
                                                     TE* __restrict__ be = nullptr,
-                                                    TE* __restrict__ xe = nullptr) {
+                                                    TE* __restrict__ xe = nullptr,
+                                                    const TE* __restrict__ ue = nullptr,
+                                                    T* __restrict__ uo = nullptr) {
   constexpr int NT = TX * TY;
   constexpr int RX = TX + 2, RY = TY + 2, PL = RX * RY;
   constexpr int UPT = (PL + NT - 1) / NT;
@@ -1042,6 +1047,12 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(u + (int64_t)m * sz);
 #pragma unroll
     for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, u_src[e], 0u);
+    if (ue) {  // u + (T) e, as the separate update pass rounds it
+      const __amdgpu_buffer_rsrc_t re = buf_rsrc(ue + (int64_t)m * sz);
+#pragma unroll
+      for (int e = 0; e < UPT; ++e)
+        up[e] = up[e] + (T)buf_load<TE>(re, (u_src[e] / TS) * (uint32_t)sizeof(TE), 0u);
+    }
   };
   auto put_plane = [&](int m) {
     T* P = ring + (m & 3) * PL;
@@ -1106,7 +1117,8 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
       if (be) {
         const int64_t p = (int64_t)m * sz + pbase + ty * sy + tx;
         be[p] = (TE)rv;
-        xe[p] = TE(0);
+        if (xe) xe[p] = TE(0);
+        if (uo) uo[p] = P0[0];
       }
       sq += (double)rv * (double)rv;
     }

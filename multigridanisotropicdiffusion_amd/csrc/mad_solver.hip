@@ -1106,8 +1106,20 @@ class Solver final : public SolverBase {
   // levels of >= 16 x 16 write the fp32 hierarchy's next rhs b = (T) r and x = 0 in the same
   // pass instead of r64 (refine_emitted_; else run_refine converts r64 and fills x)
   bool refine_emitted_ = false;
-  double residual64() {
+  // fold: u += (double) x (the fp32 cycle's correction) in the same pass -- one GPU, resid3_k levels:
+  // the updated iterate goes to the second fp64 buffer (r64_, unused by this path) and the pointers
+  // swap; x = 0 is then a separate fill (neighbouring tiles read x while the pass runs)
+  bool refine_fold_ok() const {
+    const LevelData<T>& L = lv_[0];
+    return c_->dim == 3 && L.g.nx >= 16 && L.g.ny >= 16 && !c_->geom[0].distributed;
+  }
+  double residual64(bool fold = false) {
     LevelData<T>& L = lv_[0];
+    if (fold && !refine_fold_ok()) {
+      hipLaunchKernelGGL((add_conv_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, u64_, L.x, L.g.N);
+      HIP_CHECK(hipGetLastError());
+      fold = false;
+    }
     if (c_->comm.active() && c_->geom[0].distributed) {
       wait_all_pending();
       c_->comm.exchange_planes(u64_, L.g.sz, L.g.nz, 1, L.g.zlo_ghost, L.g.zhi_ghost, sizeof(double),
@@ -1126,14 +1138,23 @@ class Solver final : public SolverBase {
       REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
       auto go = [&](auto K) {
         constexpr int KD = decltype(K)::value;
-        hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T>), dim3((unsigned)nparts), dim3(TX * TY),
-                           0, c_->stream, u64_, b64_, (double*)nullptr, cf64_, g, rat64_, zc, ntx, part_,
-                           L.b, L.x);
+        if (fold)
+          hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T>), dim3((unsigned)nparts), dim3(TX * TY),
+                             0, c_->stream, u64_, b64_, (double*)nullptr, cf64_, g, rat64_, zc, ntx, part_,
+                             L.b, (T*)nullptr, (const T*)L.x, r64_);
+        else
+          hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T>), dim3((unsigned)nparts), dim3(TX * TY),
+                             0, c_->stream, u64_, b64_, (double*)nullptr, cf64_, g, rat64_, zc, ntx, part_,
+                             L.b, L.x);
       };
       refine_emitted_ = true;
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
       else if (c_->kind == KDIAG) go(std::integral_constant<int, KDIAG>{});
       else go(std::integral_constant<int, KISO>{});
+      if (fold) {
+        std::swap(u64_, r64_);
+        hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, L.x, L.g.N, T(0));
+      }
     } else {
       dim3 gr = grid_for(g.nx, g.ny, g.nz, BLK);
       nparts = (int64_t)gr.x * gr.y * gr.z;
@@ -1799,9 +1820,8 @@ class Solver final : public SolverBase {
           if (d.verbose && c_->comm.rank() == 0) std::printf("\n|--- VCycle n. %u ---|\n", it + 1);
           vcycle_fast();
         }
-        hipLaunchKernelGGL((add_conv_k<T>), dim3(nb), dim3(256), 0, c_->stream, u64_, L0.x, N);
-        HIP_CHECK(hipGetLastError());
-        resNorm = residual64();  // MAD.hxx:221-229
+        resNorm = residual64(/*fold=*/true);  // u += e, then MAD.hxx:221-229
+
         REQUIRE(std::isfinite(resNorm), MAD_ERR_NUMERIC,
                 "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
         relres = (rhsNorm > 0.0) ? resNorm / rhsNorm : resNorm;
