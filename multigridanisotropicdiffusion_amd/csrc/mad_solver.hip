@@ -1238,6 +1238,9 @@ class Solver final : public SolverBase {
   // runs residual + restriction.
   bool residual_restrict(int l) override { return resid_restrict(l); }
   // zero_x: also zero x[l+1] (the V-cycle descent's fill, folded into the same pass)
+#ifndef MAD_RR_SMALL_VOXELS
+#define MAD_RR_SMALL_VOXELS 262144
+#endif
   bool resid_restrict(int l, bool zero_x = false) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
@@ -1267,7 +1270,10 @@ class Solver final : public SolverBase {
     auto run = [&](auto CXc, auto CYc, auto NTc) {
       constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = decltype(NTc)::value;
       const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
-      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / 4));
+      // small coarse levels: one coarse plane per workgroup (a few tiles per plane cannot fill the
+      // chip, and each z-step of the march is a serial round trip)
+      const int zdiv = C.g.N <= MAD_RR_SMALL_VOXELS ? 1 : 4;
+      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / zdiv));
       const int kc = (C.g.nz + chunks - 1) / chunks;
       chunks = (C.g.nz + kc - 1) / kc;
       const dim3 grid((unsigned)(ntx * nty * chunks)), block(NT);
