@@ -1239,7 +1239,7 @@ class Solver final : public SolverBase {
   bool residual_restrict(int l) override { return resid_restrict(l); }
   // zero_x: also zero x[l+1] (the V-cycle descent's fill, folded into the same pass)
 #ifndef MAD_RR_SMALL_VOXELS
-#define MAD_RR_SMALL_VOXELS 262144
+#define MAD_RR_SMALL_VOXELS 65536
 #endif
   bool resid_restrict(int l, bool zero_x = false) {
     LevelData<T>& F = lv_[l];
@@ -1270,8 +1270,10 @@ class Solver final : public SolverBase {
     auto run = [&](auto CXc, auto CYc, auto NTc) {
       constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = decltype(NTc)::value;
       const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
-      // small coarse levels: one coarse plane per workgroup (a few tiles per plane cannot fill the
-      // chip, and each z-step of the march is a serial round trip)
+      // small coarse levels (<= 65536 voxels): one coarse plane per workgroup (a few tiles per plane
+      // cannot fill the chip, and each z-step of the march is a serial round trip): 8^3..32^3 descents
+      // 17.7 / 19.3 / 21.3 -> 9.6 / 9.7 / 10.9 us; at 64^3 it costs (27.2 -> 36.4 us), so 4 planes stay
+      // the minimum there (profiles/r04_rr_chunk_ab.md)
       const int zdiv = C.g.N <= MAD_RR_SMALL_VOXELS ? 1 : 4;
       int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / zdiv));
       const int kc = (C.g.nz + chunks - 1) / chunks;
