@@ -8,7 +8,8 @@ bash tools/gpu_steps.sh \
   "final_gputests|1100|python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread" \
   "final_smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'" \
   "final_bench|300|python bench.py" \
-  "final_prof|900|bash tools/profile_round.sh final_prof"
+  "final_prof|900|bash tools/profile_round.sh final_prof" \
+  "final_vcycle_prof|700|bash tools/vcycle_profiles.sh"
 # (not part of the driver's run) the bench's N = 2 torchrun launch and V-cycle forms with two RCCL
 # ranks sharing the one GPU
 bash tools/gpu_steps.sh "final_rehearse|500|bash tools/rehearse_vcycles.sh"
