@@ -690,11 +690,14 @@ class Solver final : public SolverBase {
   // z-chunks of 256 planes: least chunk-overlap re-reads); fp64 full tensor 64x16 / 512 (the
   // 64x32 ring would need 186 KB of LDS); diagonal / isotropic tensors 64x16 / 1024
   struct FusedCfg {
-    int blocks = 2048;
+    int blocks = 256;
   };
+  // fp64 too (round 4): 256 workgroups -- at 512^3 one z-chunk per 64 x 16 tile column -- against
+  // the 2048 of rounds 1-3: level-0 sweep 2.30-2.38 vs 2.77-2.96 ms, V-cycle 15.7-15.9 vs 18.0-18.6 ms
+  // (512 / 1024 workgroups in between; profiles/r04_fp64_blocks_ab.log)
   static FusedCfg fused_cfg() {
     FusedCfg f;
-    if (sizeof(T) == 4) f.blocks = 256;
+    f.blocks = 256;
     return f;
   }
 
