@@ -441,8 +441,13 @@ struct PeerOut {
 // read their point's b from LDS at the u offset -- instead of one load per stage point of its colour,
 // which on the x-parity-interleaved dense b is a stride-2 access (two cache lines per wave load for
 // one line's worth of values).  The LDS then holds NP + NC planes (fp32 64 x 32 tiles: 155 KB).
+//
+// ZU (zero iterate): the sweep's input u is known to be zero (the first sweep of a correction cycle
+// whose x was zeroed, or never written, by the step before): its planes enter the LDS ring as
+// zeros instead of being loaded -- the same arithmetic on the same values, without the read, and
+// without the zero fill the caller would otherwise write first.
 template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false,
-          bool PEER = false, bool BL = false>
+          bool PEER = false, bool BL = false, bool ZU = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
@@ -643,10 +648,15 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
     }
   };
   auto load_plane = [&](int m) {
-    m = min(max(m, zlo), zhi - 1);
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
+    if constexpr (ZU) {
 #pragma unroll
-    for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, usrc[e], 0u);
+      for (int e = 0; e < UPT; ++e) up[e] = T(0);
+    } else {
+      m = min(max(m, zlo), zhi - 1);
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
+#pragma unroll
+      for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, usrc[e], 0u);
+    }
   };
   auto put_plane = [&](int m) {
     unsigned char* P = lbytes + slot(m) * (PLANE * TS);

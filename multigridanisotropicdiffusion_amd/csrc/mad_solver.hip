@@ -744,7 +744,7 @@ class Solver final : public SolverBase {
   }
 
   template <int KD, int TX, int TY, int NT>
-  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part) {
+  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part, bool zu = false) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
     int flip = 0;
@@ -788,9 +788,16 @@ class Solver final : public SolverBase {
     } else if (L.brec) {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
     } else if constexpr (bl_fits) {
-      bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true>)
-         : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+      if (zu) {  // zero iterate (zero_sweep_ok: fp32 whole-slab sweeps only)
+        REQUIRE(part == 0, MAD_ERR_STATE, "zero-iterate sweep on a rank slab");
+        bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true, true>)
+           : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, false, true>);
+      } else {
+        bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true>)
+           : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
+      }
     } else {
+      REQUIRE(!zu, MAD_ERR_STATE, "zero-iterate sweep without its instance");
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
     }
   }
@@ -814,17 +821,17 @@ class Solver final : public SolverBase {
     *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
   }
 
-  void launch_fused_part(LevelData<T>& L, int part) {
+  void launch_fused_part(LevelData<T>& L, int part, bool zu = false) {
     const FusedCfg fc = fused_cfg();
     if (c_->kind == KFULL) {
       if constexpr (sizeof(T) == 4)
-        launch_fused<KFULL, 64, 32, 1024>(L, fc, part);
+        launch_fused<KFULL, 64, 32, 1024>(L, fc, part, zu);
       else
-        launch_fused<KFULL, 64, 16, 512>(L, fc, part);
+        launch_fused<KFULL, 64, 16, 512>(L, fc, part, zu);
     } else if (c_->kind == KDIAG) {
-      launch_fused<KDIAG, 64, 16, 1024>(L, fc, part);
+      launch_fused<KDIAG, 64, 16, 1024>(L, fc, part, zu);
     } else {
-      launch_fused<KISO, 64, 16, 1024>(L, fc, part);
+      launch_fused<KISO, 64, 16, 1024>(L, fc, part, zu);
     }
     HIP_CHECK(hipGetLastError());
   }
@@ -956,9 +963,10 @@ class Solver final : public SolverBase {
                                std::is_same<T, double>::value, c_->comm_stream);
       HIP_CHECK(hipEventRecord(L.ev_halo, c_->comm_stream));
     } else if (!overlap) {
-      {
-        launch_fused_part(L, 0);
-      }
+      // the first sweep of a refine correction cycle: x is zero by construction (run_refine)
+      const bool zu = zero_x0_ && &L == &lv_[0];
+      zero_x0_ = false;
+      launch_fused_part(L, 0, zu);
     } else {
       launch_fused_part(L, 1);
       wait_all_pending();  // (none expected: halo() above already waited)
@@ -1116,6 +1124,21 @@ class Solver final : public SolverBase {
     const LevelData<T>& L = lv_[0];
     return c_->dim == 3 && L.g.nx >= 16 && L.g.ny >= 16 && !c_->geom[0].distributed;
   }
+  // zero iterate: the next V-cycle's first level-0 sweep reads x as zero without loading it
+  // (gs_fused3_k ZU), so the folded refine pass leaves x as it is instead of filling it --
+  // only where that sweep is the first thing of the cycle to touch x: a fused fp32 whole-slab
+  // sweep at level 0 of a multi-level V-cycle, with pre-smoothing, on one GPU
+  bool zero_x0_ = false;
+  bool zero_sweep_ok() const {
+#ifdef MAD_NO_ZERO_SWEEP
+    return false;
+#else
+    const auto& d = c_->d;
+    return sizeof(T) == 4 && refine_fold_ok() && !c_->comm.active() && d.cycle == MAD_VCYCLE &&
+           !d.verbose && d.iterations_per_grid >= 1 && c_->nlev > 1 && use_fused(0) && d.gs_kernel != 4 &&
+           !lv_[0].brec;
+#endif
+  }
   double residual64(bool fold = false) {
     LevelData<T>& L = lv_[0];
     if (fold && !refine_fold_ok()) {
@@ -1156,7 +1179,8 @@ class Solver final : public SolverBase {
       else go(std::integral_constant<int, KISO>{});
       if (fold) {
         std::swap(u64_, r64_);
-        hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, L.x, L.g.N, T(0));
+        if (!zero_sweep_ok())
+          hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, L.x, L.g.N, T(0));
       }
     } else {
       dim3 gr = grid_for(g.nx, g.ny, g.nz, BLK);
@@ -1510,12 +1534,13 @@ class Solver final : public SolverBase {
     }
     sync_brec(0);  // eager: level 0's b changes between cycles (time steps), not inside
     if (ranks) ranks_graph_entry();
+    const bool zu = zero_x0_;  // the graph bakes in the first sweep's zero-iterate form too
     if (vgraph_) {
       // the graph baked in every level's x / t buffers: a call between two cycles that
       // swapped a ping-pong pair an odd number of times (mad_smooth with an odd sweep
       // count under WJ, or of the fused GS sweep) leaves it pointing at stale buffers,
       // so it is re-captured for the current pointers
-      bool same = vgraph_ptrs_.size() == lv_.size();
+      bool same = vgraph_ptrs_.size() == lv_.size() && vgraph_zu_ == zu;
       for (size_t l = 0; same && l < lv_.size(); ++l)
         same = vgraph_ptrs_[l].first == lv_[l].x && vgraph_ptrs_[l].second == lv_[l].t;
       if (!same) {
@@ -1588,16 +1613,20 @@ class Solver final : public SolverBase {
         same = false;
       }
       if (gph) (void)hipGraphDestroy(gph);
+      zero_x0_ = zu;  // (consumed by the capture)
       if (!same) {
         (void)hipGetLastError();
         vgraph_failed_ = true;
         vcycle_rec(0);
         return;
       }
+      vgraph_zu_ = zu;
+      zero_x0_ = false;
       vgraph_ptrs_.clear();
       for (auto& L : lv_) vgraph_ptrs_.emplace_back(L.x, L.t);
     }
     HIP_CHECK(hipGraphLaunch(vgraph_, c_->stream));
+    zero_x0_ = false;
     if (ranks) c_->comm.graph_launched(c_->stream);
     if (ranks) {
       for (size_t l = 0; l < lv_.size(); ++l) {
@@ -1829,7 +1858,9 @@ class Solver final : public SolverBase {
           smooth(0, 1);
         } else {
           if (d.verbose && c_->comm.rank() == 0) std::printf("\n|--- VCycle n. %u ---|\n", it + 1);
+          zero_x0_ = refine_emitted_ && zero_sweep_ok();  // x = 0 (or left stale by the fold)
           vcycle_fast();
+          zero_x0_ = false;
         }
         resNorm = residual64(/*fold=*/true);  // u += e, then MAD.hxx:221-229
 
@@ -1985,6 +2016,7 @@ class Solver final : public SolverBase {
   Rat<double> rat64_{};
   int64_t part_cap_ = 0;             // entries of part_
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
+  bool vgraph_zu_ = false;            // its first level-0 sweep is the zero-iterate form
   std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
   bool vgraph_failed_ = false;
   uint64_t peer_timeout_ticks_ = 0;

@@ -193,3 +193,25 @@ def test_refine_rank_slabs_match_single(M):
     assert rst["last_relres"] <= 1e-10
     assert np.abs(full - ref).max() <= 1e-12 * np.abs(ref).max()
     assert all(list(o[1]["step_cycles"]) == list(rst["step_cycles"]) for o in outs)
+
+
+@pytest.mark.parametrize("gs_kernel", [0, 3])
+def test_zero_iterate_first_sweep_is_bitwise(M, gs_kernel):
+    """The refine correction cycle's first level-0 sweep takes x as zero without loading it
+    (gs_fused3_k ZU), and the folded fp64 pass then skips the x = 0 fill: a verbose run (eager
+    cycles, the plain sweep on the filled x) gives the same iterate bit for bit and the same
+    cycle counts.  gs_kernel 0 at 160^3 (the auto rule's fused level 0), 3 forces it at 64^3."""
+    shape = (160, 160, 160) if gs_kernel == 0 else (64, 64, 64)
+    T = synth.ved_form(shape)
+    img = synth.image(shape, seed=7) * 100
+    outs = []
+    for verbose in (False, True):
+        s = M.Solver(shape, time_step=0.4, tolerance=1e-10, precision=M.FP32_REFINE, number_of_steps=2,
+                     gs_kernel=gs_kernel, verbose=verbose)
+        s.set_tensor(T)
+        outs.append(s.run(img, out_dtype=np.float64))
+        s.close()
+    (a, sa), (b, sb) = outs
+    assert sa["last_relres"] <= 1e-10
+    assert list(sa["step_cycles"]) == list(sb["step_cycles"])
+    assert np.array_equal(a, b)
