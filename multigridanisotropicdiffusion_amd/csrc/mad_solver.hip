@@ -857,8 +857,9 @@ class Solver final : public SolverBase {
       const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : 1024;
       const bool brec = lv_[l].brec;
       const LevelData<T>& L = lv_[l];
-      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER, BL last)
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s, %s>", tn, kind, tx, ty,
+      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER, BL, ZU last; the
+      // zero-iterate form is only the first sweep of a refine correction cycle)
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s, %s, false>", tn, kind, tx, ty,
                     nt, sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false", L.peer ? "true" : "false",
                     fused_b_lds(L) ? "true" : "false");
       // rank slabs: which sweep form fused_sweep takes

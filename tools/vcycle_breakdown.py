@@ -31,7 +31,7 @@ def main():
     fam = defaultdict(lambda: [0, 0.0])
     for e in sel:
         short = e[2].split("(")[0].replace("void ", "")
-        k = (short[:70], e[3])
+        k = (short[:90], e[3])
         fam[k][0] += 1
         fam[k][1] += (e[1] - e[0]) / 1e6
     print("| kernel | grid | launches/cycle | ms/cycle | us/launch |")
