@@ -1,6 +1,8 @@
 # zero-iterate first sweep of the refine correction cycle (gs_fused3_k ZU, no x = 0 fill): refine tests
 # vs the oracle, bitwise equality of a whole mad_run with a -DMAD_NO_ZERO_SWEEP build
-# (tools/pglibs/libmad_nozero.so), then the bench's per-cycle costs alternated
+# (tools/pglibs/libmad_nozero.so), then the bench's per-cycle costs alternated.  Build that library first, here:
+#   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DMAD_NO_ZERO_SWEEP -o tools/pglibs/libmad_nozero.so \
+#     multigridanisotropicdiffusion_amd/csrc/mad_solver.hip -lrccl -lrocsolver -lrocblas
 set -o pipefail
 timeout -k 10 500 python -u -m pytest tests/test_gpu_refine.py -m gpu -x -q --timeout 300 --timeout-method thread && \
 timeout -k 10 120 python -u tools/refine_fold_ab.py /tmp/zu_new.npy && \
