@@ -3,16 +3,19 @@
     python tests/golden/make_golden.py
 
 Inputs
-  lena_256_u8.npy   centre 256x256 crop of the reference's test/test_data/lena.jpg
-                    (decoded with PIL; the reference reads it as unsigned char,
-                    test/itk2DDiffusionTest_GS.cxx:21-42)
+  lena_512_u8.npy   the reference's whole test/test_data/lena.jpg (512x512, grayscale JPEG),
+                    decoded once with PIL; the reference reads it as unsigned char
+                    (test/itk2DDiffusionTest_GS.cxx:21-42) -- the input of the nine ctest
+                    registrations (tests/test_gpu_registrations.py)
+  lena_256_u8.npy   centre 256x256 crop of it (BASELINE config C1)
   ved_crop_i16.npy  35x39x35 crop (z,y,x) of test/test_data/ved_test.zraw (zlib,
                     int16, DimSize 69 77 69, spacing .3125 .3125 .5)
   ved2_crop_i16.npy 55x52x54 centre crop (z,y,x) of test/test_data/ved_test_2.zraw (zlib,
                     int16, DimSize 134 140 119, spacing .330017): its hierarchy coarsens
                     CCV -> VCC -> CVC (x,y,z), the first three of the full volume's
                     CCV -> VCC -> CVC -> VCV
-  (python tests/golden/make_golden.py ved2   regenerates only the ved_test_2 fixtures,
+  (python tests/golden/make_golden.py lena512 writes only lena_512_u8.npy,
+   python tests/golden/make_golden.py ved2   regenerates only the ved_test_2 fixtures,
    python tests/golden/make_golden.py lena64 only the fp64 lena solutions lena_c1_f64.npz)
 Expected outputs come from the fp64 oracle (oracle/), which restates the
 reference line by line.  PARITY UNPINNED: the reference has no golden vectors
@@ -39,6 +42,7 @@ REF = "/root/reference/test/test_data"
 def make_inputs():
     from PIL import Image
     lena = np.asarray(Image.open(os.path.join(REF, "lena.jpg")).convert("L"))
+    np.save(os.path.join(HERE, "lena_512_u8.npy"), np.ascontiguousarray(lena))
     c0 = (lena.shape[0] - 256) // 2
     np.save(os.path.join(HERE, "lena_256_u8.npy"), np.ascontiguousarray(lena[c0:c0 + 256, c0:c0 + 256]))
     raw = zlib.decompress(open(os.path.join(REF, "ved_test.zraw"), "rb").read())
@@ -130,7 +134,17 @@ def lena_f64():
     np.savez_compressed(os.path.join(HERE, "lena_c1_f64.npz"), **res)
 
 
+def make_lena512():
+    from PIL import Image
+    lena = np.asarray(Image.open(os.path.join(REF, "lena.jpg")).convert("L"))
+    assert lena.shape == (512, 512) and lena.dtype == np.uint8
+    np.save(os.path.join(HERE, "lena_512_u8.npy"), np.ascontiguousarray(lena))
+
+
 def main():
+    if sys.argv[1:] == ["lena512"]:
+        make_lena512()
+        return
     if sys.argv[1:] == ["lena64"]:
         lena_f64()
         return

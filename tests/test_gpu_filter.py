@@ -42,8 +42,12 @@ def lena_tensor(shape):
 ])
 @pytest.mark.parametrize("precision", ["FP32", "FP64", "PRECISION_AUTO"])
 def test_itk2d_diffusion(M, lena, smoother, cycle, key, precision):
-    """itk2DDiffusionTest_{GS,WJ}_{V,FMG,S} on the 256x256 lena crop: float input,
-    IterationsPerGrid 2, TimeStep 0.1, 1 step, MaxCycles 100, Tolerance 1e-10."""
+    """BASELINE config C1: the itk2DDiffusionTest_{GS,WJ} parameters (float input,
+    IterationsPerGrid 2, TimeStep 0.1, 1 step, MaxCycles 100, Tolerance 1e-10) on the 256x256
+    lena crop, against the committed oracle goldens.  CHANGED PARAMETER, on purpose: the WJ
+    SMOOTHER case runs MaxCycles 20000 so the plain smoother converges and is compared with the
+    converged V-cycle golden (a smoother-convergence check); the registrations as registered
+    -- whole 512^2 lena, _S stopped at MaxCycles 100 -- are tests/test_gpu_registrations.py."""
     golden = load_golden("lena_c1")
     sm = M.MultigridWeightedJacobiSmoother if smoother == "WJ" else M.MultigridGaussSeidelSmoother
     f = M.MultigridAnisotropicDiffusionImageFilter(smoother=sm, output_dtype=np.float32,

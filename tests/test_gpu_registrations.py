@@ -1,0 +1,306 @@
+"""The reference's nine ctest registrations, run as registered, against the oracle.
+
+test/CMakeLists.txt:14-44 registers
+
+    itk2DDiffusionTest_GS_FMG  itk2DDiffusionTest_GS_V  itk2DDiffusionTest_WJ_FMG
+    itk2DDiffusionTest_WJ_V    itk2DDiffusionTest_GS_S  itk2DDiffusionTest_WJ_S
+    itkVEDTest_GS_V            itkVEDTest_GS_FMG        itkVEDTest_GS_S
+
+Each runs here on the registration's own input and parameters, through the ITK-shaped
+facade, and is compared with the fp64 oracle (oracle/, the restated reference) run with
+the same parameters:
+
+* 2D (test/itk2DDiffusionTest_{GS,WJ}.cxx): the WHOLE 512x512 test_data/lena.jpg as
+  unsigned char (tests/golden/lena_512_u8.npy, decoded once with PIL by
+  tests/golden/make_golden.py), cast to float; tensor M = [[50, 0], [0, 30]] everywhere
+  (:65-70); IterationsPerGrid 2, Verbose, TimeStep 0.1, NumberOfSteps 1, MaxCycles 100,
+  Tolerance 1e-10 (:92-97); CycleType from argv[1] (:102-107).  The weighted-Jacobi
+  program differs only in the smoother (itk2DDiffusionTest_WJ.cxx).
+* VED (test/itkVEDTest_GS.cxx): test_data/ved_test.mhd (short), scales .3 .482 .775 1.245
+  2, alpha .5, beta .5, gamma 5, epsilon .01, sensitivity 10, 1 iteration, Tolerance 1e-10,
+  TimeStep 0.1, 4 diffusion iterations, 3 iterations per grid, omega 1.5 (:61-92); the
+  diffusion step is a MAD filter with MaxCycles 100 (include/itkVEDMultigridImageFilter.hxx:
+  381-402).
+
+No reference parameter is changed.  In particular the 2D SMOOTHER (_S) registrations stop
+after MaxCycles = 100 sweeps, unconverged (MAD.hxx:207-246: relres ~3e-4 for WJ, ~5e-8 for
+GS on lena), so their output depends on the sweep ORDER, not only on the linear system
+(itkVEDTest_GS_S's small time step converges in ~50 sweeps per diffusion step, below
+MaxCycles):
+
+* WJ_S: the weighted-Jacobi sweep is order-free, so the GPU's 100 sweeps are compared with
+  the oracle's 100 sweeps directly.
+* GS_S: the reference's GS is lexicographic (itkMultigridGaussSeidelSmoother.hxx:67-106).
+  The GPU's default GS (MultigridGaussSeidelSmoother) is multicolour -- a DIFFERENT sweep
+  order, whose 100-sweep iterate is a different unconverged vector.  So GS_S runs (1) with
+  the reference's order, MultigridGaussSeidelLexSmoother (MAD_GAUSS_SEIDEL_LEX, hyperplane
+  wavefronts), against the oracle's lexicographic sweeps, and (2) with the default
+  multicolour smoother against the oracle's multicolour sweeps of the same colouring
+  (2 colours: the lena tensor is diagonal; 4 for VED's full tensors).
+* The V / FMG registrations converge to Tolerance 1e-10, where the sweep order no longer
+  matters: the converged bounds (north star 1e-5 in fp32; 1e-7 with the default precision
+  and in fp64, different smoother orders; 1e-9 with the same order in fp64).
+
+Output pixel type: the 2D programs write float (ImageType float, :26); the comparisons read
+the solution as fp64 (the filter's internal type) so the fp64 bounds are not limited by
+the output cast.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import synth
+import ved_oracle as VO
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def relinf(a, ref):
+    return np.abs(np.asarray(a, np.float64) - ref).max() / np.abs(ref).max()
+
+
+@pytest.fixture(scope="module")
+def M():
+    import multigridanisotropicdiffusion_amd as mod
+    return mod
+
+
+# ----------------------------------------------------------------------------- 2D (lena)
+@pytest.fixture(scope="module")
+def lena512():
+    img = np.load(os.path.join(GOLDEN, "lena_512_u8.npy"))
+    assert img.shape == (512, 512) and img.dtype == np.uint8
+    return img
+
+
+def lena_tensor(shape):
+    # Space-independent anisotropic tensor M = [[50, 0], [0, 30]] (itk2DDiffusionTest_GS.cxx:65-70)
+    return np.stack([np.full(shape, 50.0), np.zeros(shape), np.full(shape, 30.0)], axis=0)
+
+
+@pytest.fixture(scope="module")
+def lena_oracle(oracle_mod, lena512):
+    """fp64 oracle GenerateData with the registration's parameters, cached per
+    (smoother, cycle)."""
+    x = lena512.astype(np.float32).astype(np.float64)  # CastImageFilter<uchar, float> (:37-42)
+    o = oracle_mod.Oracle(x.shape, (1.0, 1.0), lena_tensor(x.shape), 0.1)
+    cache = {}
+
+    def get(smoother, cycle, ncolors=0):
+        key = (smoother, cycle, ncolors)
+        if key not in cache:
+            cache[key] = o.run(x, cycle=cycle, smoother=smoother, iterations_per_grid=2,
+                               max_cycles=100, number_of_steps=1, tolerance=1e-10,
+                               ncolors=ncolors)
+        return cache[key]
+    return get
+
+
+def run_2d(M, img, smoother_cls, cycle, precision):
+    """itk2DDiffusionTest_{GS,WJ}.cxx:88-109, through the facade."""
+    f = M.MultigridAnisotropicDiffusionImageFilter(smoother=smoother_cls, output_dtype=np.float64,
+                                                   precision=getattr(M, precision))
+    f.SetInput(M.Image(img.astype(np.float32)))  # CastImageFilter< uchar -> float >
+    f.SetDiffusionTensor(lena_tensor(img.shape).transpose(1, 2, 0))
+    f.SetIterationsPerGrid(2)
+    f.SetVerbose(True)
+    f.SetTimeStep(0.1)
+    f.SetNumberOfSteps(1)
+    f.SetMaxCycles(100)
+    f.SetTolerance(1e-10)
+    f.SetCycle({"V": f.VCYCLE, "FMG": f.FMG, "S": f.SMOOTHER}[cycle])
+    f.Update()
+    return f.GetOutput().GetBufferAsArray(), f.stats
+
+
+PRECISIONS = ["FP32", "FP64", "PRECISION_AUTO"]
+
+
+@pytest.mark.parametrize("cycle", ["FMG", "V"])
+@pytest.mark.parametrize("smoother", ["GS", "WJ"])
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_itk2d_diffusion_converging_registrations(M, oracle_mod, lena512, lena_oracle,
+                                                  smoother, cycle, precision):
+    """itk2DDiffusionTest_{GS,WJ}_{FMG,V}: solve to Tolerance 1e-10 within MaxCycles 100.
+    GS: the GPU's multicolour GS against the reference's lexicographic GS (both converged);
+    WJ: the same iteration as the reference's, so in fp64 the same cycle count."""
+    sm_gpu = M.MultigridWeightedJacobiSmoother if smoother == "WJ" else M.MultigridGaussSeidelSmoother
+    sm_ora = oracle_mod.WJ if smoother == "WJ" else oracle_mod.GS_LEX
+    ocyc = oracle_mod.FMG if cycle == "FMG" else oracle_mod.VCYCLE
+    ref, ocycles, orr = lena_oracle(sm_ora, ocyc)
+    assert orr[0] <= 1e-10  # the oracle itself converges within MaxCycles 100
+    out, st = run_2d(M, lena512, sm_gpu, cycle, precision)
+    print(f"{smoother}_{cycle} {precision}: cycles {st['step_cycles']} (oracle {ocycles}) relres "
+          f"{st['last_relres']:.3e}, rel err {relinf(out, ref):.2e}")
+    assert st["steps"] == 1 and st["total_cycles"] <= 100
+    if precision == "FP32":
+        # plain fp32 ends at its rounding floor (~1e-7, the stall guard) above 1e-10
+        assert relinf(out, ref) < 1e-5
+        return
+    # FP64, and the default (PRECISION_AUTO -> FP32_REFINE at 1e-10), reach the tolerance
+    assert st["last_relres"] <= 1e-10 and st["converged"]
+    same_order = smoother == "WJ" and precision == "FP64"
+    assert relinf(out, ref) < (1e-9 if same_order else 1e-7)
+    if same_order:
+        assert st["step_cycles"] == ocycles
+
+
+@pytest.mark.parametrize("cycle", ["FMG", "V"])
+def test_itk2d_gs_registrations_in_the_reference_order(M, oracle_mod, lena512, lena_oracle, cycle):
+    """itk2DDiffusionTest_GS_{FMG,V} with the reference's lexicographic order
+    (MultigridGaussSeidelLexSmoother) in fp64: the reference's iteration, so the same cycle
+    count and the solution to 1e-9."""
+    ocyc = oracle_mod.FMG if cycle == "FMG" else oracle_mod.VCYCLE
+    ref, ocycles, _ = lena_oracle(oracle_mod.GS_LEX, ocyc)
+    out, st = run_2d(M, lena512, M.MultigridGaussSeidelLexSmoother, cycle, "FP64")
+    print(f"GS_{cycle} lex FP64: cycles {st['step_cycles']} (oracle {ocycles}), rel err {relinf(out, ref):.2e}")
+    assert st["step_cycles"] == ocycles and st["last_relres"] <= 1e-10
+    assert relinf(out, ref) < 1e-9
+
+
+# WJ_S / GS_S: 100 sweeps from u = b, stopped at MaxCycles (relres ~3e-4 / ~5e-8)
+S_BOUNDS = {
+    # (precision): bound on ||u_gpu - u_oracle||_inf / ||u_oracle||_inf after 100 sweeps
+    "FP64": 1e-12,            # same arithmetic order per point as the oracle: rounding only
+    "FP32": 1e-5,             # fp32 storage / arithmetic over 100 sweeps (north-star bar)
+    "PRECISION_AUTO": 1e-6,   # FP32_REFINE: u + S(0; b - Au), fp32 corrections of fp64 u
+}
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_itk2d_diffusion_wj_s(M, oracle_mod, lena512, lena_oracle, precision):
+    """itk2DDiffusionTest_WJ_S: 100 weighted-Jacobi sweeps (omega 2/3), stopped unconverged
+    at MaxCycles 100, exactly as registered."""
+    ref, ocycles, orr = lena_oracle(oracle_mod.WJ, oracle_mod.SMOOTHER)
+    assert ocycles == [100] and orr[0] > 1e-10
+    out, st = run_2d(M, lena512, M.MultigridWeightedJacobiSmoother, "S", precision)
+    print(f"WJ_S {precision}: relres {st['last_relres']:.3e} (oracle {orr[0]:.3e}), "
+          f"rel err {relinf(out, ref):.2e}")
+    assert st["step_cycles"] == [100]
+    assert relinf(out, ref) < S_BOUNDS[precision]
+    # the same unconverged relres (the reference's loop condition, MAD.hxx:246)
+    assert abs(st["last_relres"] - orr[0]) < 1e-3 * orr[0]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_itk2d_diffusion_gs_s_reference_order(M, oracle_mod, lena512, lena_oracle, precision):
+    """itk2DDiffusionTest_GS_S in the reference's lexicographic order
+    (MultigridGaussSeidelLexSmoother): 100 sweeps, stopped at MaxCycles 100, against the
+    oracle's 100 lexicographic sweeps."""
+    ref, ocycles, orr = lena_oracle(oracle_mod.GS_LEX, oracle_mod.SMOOTHER)
+    assert ocycles == [100] and orr[0] > 1e-10
+    out, st = run_2d(M, lena512, M.MultigridGaussSeidelLexSmoother, "S", precision)
+    print(f"GS_S lex {precision}: cycles {st['step_cycles']} relres {st['last_relres']:.3e} "
+          f"(oracle {orr[0]:.3e}), rel err {relinf(out, ref):.2e}")
+    bound = {"FP64": 1e-10, "FP32": 1e-5, "PRECISION_AUTO": 1e-6}[precision]
+    assert relinf(out, ref) < bound
+    if precision != "FP32":
+        assert st["step_cycles"] == [100]
+        assert abs(st["last_relres"] - orr[0]) < 1e-2 * orr[0]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_itk2d_diffusion_gs_s_multicolour(M, oracle_mod, lena512, lena_oracle, precision):
+    """itk2DDiffusionTest_GS_S with the default (multicolour) GS: a different sweep order
+    from the reference's, so its 100-sweep iterate is compared with the oracle's 100
+    red-black sweeps (the lena tensor is diagonal: 5-point stencil, 2 colours).  Against the
+    reference's lexicographic iterate it differs by the sweep order (asserted only to be of
+    the same unconverged quality)."""
+    ref, ocycles, orr = lena_oracle(oracle_mod.GS_COLOR, oracle_mod.SMOOTHER, ncolors=2)
+    lex, _, lrr = lena_oracle(oracle_mod.GS_LEX, oracle_mod.SMOOTHER)
+    out, st = run_2d(M, lena512, M.MultigridGaussSeidelSmoother, "S", precision)
+    print(f"GS_S multicolour {precision}: cycles {st['step_cycles']} relres {st['last_relres']:.3e} "
+          f"(oracle {orr[0]:.3e}, lex {lrr[0]:.3e}), rel err {relinf(out, ref):.2e}, vs lex "
+          f"{relinf(out, lex):.2e}")
+    assert st["colors"] == 2
+    bound = {"FP64": 1e-12, "FP32": 1e-5, "PRECISION_AUTO": 1e-6}[precision]
+    assert relinf(out, ref) < bound
+    if precision != "FP32":
+        assert st["step_cycles"] == [100]
+        assert abs(st["last_relres"] - orr[0]) < 1e-2 * orr[0]
+        assert 0.1 < st["last_relres"] / lrr[0] < 10.0
+    assert relinf(out, lex) < 1e-4
+
+
+# ----------------------------------------------------------------------------- VED (ved_test)
+VED_TEST_KW = dict(alpha=0.5, beta=0.5, gamma=5.0, epsilon=0.01, sensitivity=10.0, omega=1.5,
+                   iterations=1, diffusion_iterations=4, diffusion_iterations_per_grid=3,
+                   time_step=0.1, tolerance=1e-10, scales=(0.300, 0.482, 0.775, 1.245, 2.000))
+
+
+@pytest.fixture(scope="module")
+def ved_volume():
+    from multigridanisotropicdiffusion_amd import mhd
+    arr, info = mhd.read_mhd(os.path.join(GOLDEN, "ved_test.mhd"))
+    return arr, tuple(info["spacing"])
+
+
+@pytest.fixture(scope="module")
+def ved_tensor_ref(ved_volume):
+    """GenerateDiffusionTensor of the oracle (fp64, LAPACK eigen-analysis), once."""
+    img, sp = ved_volume
+    k = VED_TEST_KW
+    T, _ = VO.ved_tensor(img.astype(np.float64), sp, k["scales"], k["alpha"], k["beta"],
+                         k["gamma"], k["epsilon"], k["omega"], k["sensitivity"])
+    return T
+
+
+def ved_diffuse_oracle(oracle_mod, img, sp, T, cycle, smoother, ncolors=0):
+    """DiffusionStep (VED.hxx:381-402): a MAD filter, MaxCycles 100, on tensor T."""
+    k = VED_TEST_KW
+    o = oracle_mod.Oracle(img.shape, sp, T, k["time_step"])
+    out, cyc, rr = o.run(img.astype(np.float64), cycle=cycle, smoother=smoother,
+                         iterations_per_grid=k["diffusion_iterations_per_grid"], max_cycles=100,
+                         number_of_steps=k["diffusion_iterations"], tolerance=k["tolerance"],
+                         ncolors=ncolors)
+    return out, cyc, rr
+
+
+@pytest.mark.parametrize("cycle", ["V", "FMG", "S"])
+@pytest.mark.parametrize("precision", ["FP64", "FP32"])
+def test_ved_registrations(M, oracle_mod, ved_volume, ved_tensor_ref, cycle, precision):
+    """itkVEDTest_GS_{V,FMG,S} on test_data/ved_test.mhd with the registration's parameters.
+
+    fp64: the whole filter against the oracle's whole filter (tensor from the oracle's
+    LAPACK eigen-analysis; the GPU's Jacobi eigen-analysis agrees to ~1e-13): V / FMG
+    converge to 1e-10 per diffusion step (bound 1e-8, different GS orders); S (plain sweeps,
+    converging in ~50 per step, within MaxCycles 100) runs in the reference's lexicographic
+    order (MultigridGaussSeidelLexSmoother) against the oracle's, and with the default
+    multicolour order against the oracle's 4-colour sweeps (the VED tensor is full: 19-point
+    stencil) -- the same sweep counts in fp64.
+    fp32: the tensor's strict argmax over scales (VED.hxx:272) can pick the other scale at
+    near-ties an fp32 Hessian cannot resolve (tests/test_gpu_ved.py), so the diffusion --
+    the hot path -- is compared with the oracle run on the GPU's own tensor, north-star 1e-5.
+    Short output: the truncation of the same values (VED.hxx:145), |diff| <= 1."""
+    img, sp = ved_volume
+    gcyc = {"V": M.VCYCLE, "FMG": M.FMG, "S": M.SMOOTHER}[cycle]
+    ocyc = {"V": oracle_mod.VCYCLE, "FMG": oracle_mod.FMG, "S": oracle_mod.SMOOTHER}[cycle]
+    variants = [(M.GAUSS_SEIDEL_LEX, oracle_mod.GS_LEX, 0)] if cycle == "S" else []
+    variants.append((M.GAUSS_SEIDEL, oracle_mod.GS_COLOR if cycle == "S" else oracle_mod.GS_LEX,
+                     4 if cycle == "S" else 0))
+    for sm_gpu, sm_ora, nc in variants:
+        v = M.VED(img.shape, sp, precision=getattr(M, precision), cycle=gcyc, smoother=sm_gpu,
+                  **VED_TEST_KW)
+        out, st = v.run(img, out_dtype=np.float64)
+        assert st["iterations"] == 1
+        T = ved_tensor_ref
+        if precision == "FP32":
+            T, _ = v.tensor(img)
+        ref, ocycles, _ = ved_diffuse_oracle(oracle_mod, img, sp, T, ocyc, sm_ora, nc)
+        # (ved_test's diffusion steps converge within MaxCycles in every mode: S takes ~50
+        # sweeps per step, so here the smoother order changes only the converged iterate's
+        # rounding -- the same-order comparison still takes the same sweep counts)
+        assert all(c <= 100 for c in ocycles)
+        if precision == "FP64" and cycle == "S":
+            assert st["total_cycles"] == sum(ocycles), (st["total_cycles"], ocycles)
+        err = relinf(out, ref)
+        print(f"VED {cycle} {precision} smoother {sm_gpu}: cycles {st['total_cycles']} "
+              f"(oracle {ocycles}), rel err {err:.2e}")
+        bound = 1e-5 if precision == "FP32" else 1e-8
+        assert err < bound, (sm_gpu, err)
+        out16, _ = v.run(img, out_dtype=np.int16)
+        assert out16.dtype == np.int16
+        assert np.abs(out16.astype(np.float64) - np.trunc(ref)).max() <= 1
+        v.close()
