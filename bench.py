@@ -48,10 +48,16 @@ def parse():
     p.add_argument("--cpu-size", type=int, default=0,
                    help="volume of the CPU baseline (default: the benched size)")
     p.add_argument("--no-precision-cycles", action="store_true")
-    p.add_argument("--halo", default="peer", choices=["peer", "rccl"],
-                   help="rank slabs (N > 1): 'peer' -- the fused level-0 sweep stores its edge planes "
-                        "into the neighbours' mailboxes while it runs (MAD_OPT_PEER_HALO); 'rccl' -- a "
-                        "grouped ncclSend / ncclRecv exchange after each sweep")
+    p.add_argument("--cpu-baseline-only", action="store_true",
+                   help="(internal) print cpu_baseline(--cpu-seconds, --cpu-size) as JSON and exit")
+    p.add_argument("--cpu-timeout", type=float, default=300.0,
+                   help="bound of the CPU leg at the benched size (then the 128^3 fallback)")
+    p.add_argument("--halo", default="rccl", choices=["peer", "rccl"],
+                   help="rank slabs (N > 1): 'rccl' (default) -- a grouped ncclSend / ncclRecv "
+                        "exchange after each sweep; 'peer' -- the fused level-0 sweep stores its edge "
+                        "planes into the neighbours' mailboxes while it runs (MAD_OPT_PEER_HALO; not the "
+                        "default until a one-process-per-GPU run has shown it bitwise equal to the "
+                        "in-process transport, tests/test_gpu_multiproc.py)")
     return p.parse_args()
 
 
@@ -143,6 +149,66 @@ def cpu_baseline(seconds, size):
     return out
 
 
+# peak host memory of cpu_baseline() per voxel of the benched volume (the oracle's GridsHierarchy:
+# 27 fp64 DCA stencil entries per voxel over all levels, the fp64 tensor and image arrays);
+# measured 352 B at 160^3 including the interpreter
+ORACLE_BYTES_PER_VOXEL = 360.0
+CPU_FALLBACK_SIZE = 128
+
+
+def host_mem_available():
+    """MemAvailable of /proc/meminfo in bytes (None where it cannot be read)."""
+    try:
+        with open("/proc/meminfo") as f:
+            for ln in f:
+                if ln.startswith("MemAvailable:"):
+                    return int(ln.split()[1]) * 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
+def _cpu_child(seconds, size, timeout):
+    """cpu_baseline(seconds, size) in a child process bounded by `timeout` seconds (the oracle
+    holds no GPU state; an out-of-memory kill or a hang ends the child, not the bench line).
+    Returns (result dict, None) or (None, reason)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--cpu-size", str(size),
+           "--cpu-seconds", str(seconds)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    except subprocess.TimeoutExpired:
+        return None, f"the {size}^3 CPU baseline exceeded its {timeout:.0f} s bound"
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return None, f"the {size}^3 CPU baseline exited {r.returncode} ({r.stderr.strip()[-200:]})"
+    return json.loads(lines[-1]), None
+
+
+def cpu_baseline_guarded(seconds, size, timeout=300.0, fallback_timeout=120.0, mem_available=None,
+                         fallback_size=CPU_FALLBACK_SIZE):
+    """The CPU leg, unable to cost the GPU line: the benched size when the host has 1.5x the
+    oracle's memory free and the run ends within `timeout`; otherwise the 128^3 sample, with
+    `fallback` naming the reason (and `value` None with `error` if that fails too)."""
+    need = ORACLE_BYTES_PER_VOXEL * float(size) ** 3
+    avail = host_mem_available() if mem_available is None else mem_available
+    if avail is not None and avail < 1.5 * need:
+        reason = (f"MemAvailable {avail / 2**30:.1f} GiB < 1.5 x the {need / 2**30:.1f} GiB "
+                  f"the {size}^3 oracle needs")
+    else:
+        res, reason = _cpu_child(seconds, size, timeout)
+        if res is not None:
+            return res
+    fb = min(size, fallback_size)
+    res, err = _cpu_child(seconds, fb, fallback_timeout)
+    if res is None:
+        return {"value": None, "unit": "Mvoxel-smooths/s", "cores": 1, "kind": "port",
+                "error": f"{reason}; fallback: {err}"}
+    res["fallback"] = reason
+    res["sample"] = f"FALLBACK to {fb}^3 ({reason}): " + res["sample"]
+    return res
+
+
 def run_cycle_ms(M, shape, prec, cycles, **kw):
     """Milliseconds per solver cycle inside mad_run (the reference's loop: cycle, fp64 residual,
     host convergence check; MAD.hxx:207-246) at Tolerance 1e-30, so every run takes `cycles`
@@ -186,6 +252,9 @@ def phase(rank, what):
 
 def main():
     a = parse()
+    if a.cpu_baseline_only:  # the child of cpu_baseline_guarded: no GPU, no torch
+        print(json.dumps(cpu_baseline(a.cpu_seconds, a.cpu_size or a.size)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -360,7 +429,7 @@ def main():
                                     "the reference tests' 1e-10")
     if world == 1 and not a.no_cpu_baseline:
         phase(rank, "CPU baseline (oracle)")
-        cb = cpu_baseline(a.cpu_seconds, a.cpu_size or S)
+        cb = cpu_baseline_guarded(a.cpu_seconds, a.cpu_size or S, timeout=a.cpu_timeout)
         line["cpu_baseline"] = cb
     else:
         line["cpu_baseline"] = None

@@ -23,6 +23,26 @@ def test_cpu_baseline_leg_reports_the_oracle():
     assert cb["sample_128"]["value"] > 0 and "128^3" in cb["sample_128"]["sample"]
 
 
+def test_cpu_baseline_falls_back_when_host_memory_is_short():
+    """The 512^3 oracle needs ~47 GB of host memory: below 1.5x that in MemAvailable the leg
+    runs the small sample instead, and says why, so the GPU line is never lost to it."""
+    sys.path.insert(0, ROOT)
+    import bench
+    cb = bench.cpu_baseline_guarded(0.05, 512, mem_available=8 << 30, fallback_size=24)
+    assert cb["value"] > 0 and "MemAvailable" in cb["fallback"]
+    assert cb["sample"].startswith("FALLBACK to 24^3") and "24^3" in cb["sample"]
+
+
+def test_cpu_baseline_falls_back_when_over_its_time_bound():
+    sys.path.insert(0, ROOT)
+    import bench
+    cb = bench.cpu_baseline_guarded(0.05, 40, timeout=0.01, fallback_size=24)
+    assert cb["value"] > 0 and "bound" in cb["fallback"] and cb["sample"].startswith("FALLBACK to 24^3")
+    # both legs failing still returns a line (value None, the reasons in `error`)
+    cb = bench.cpu_baseline_guarded(0.05, 40, timeout=0.01, fallback_timeout=0.01, fallback_size=24)
+    assert cb["value"] is None and "bound" in cb["error"]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("extra", [[], ["--smoother", "wj"], ["--gs-kernel", "1"]])
 def test_bench_json_line(extra):
