@@ -85,6 +85,9 @@ typedef enum mad_precision {
 /* defaults of mad_desc.coarse_dense_max / coarse_block_unknowns (the DirectSolver, DS.hxx:32-147) */
 #define MAD_COARSE_DENSE_MAX 8192
 #define MAD_COARSE_BLOCK_UNKNOWNS 2048
+/* the largest coarse_dense_max mad_create accepts (a dense inverse of n unknowns: 8 n^2 bytes of
+   host memory, 16 n^2 of device memory, checked against hipMemGetInfo at setup) */
+#define MAD_COARSE_DENSE_LIMIT 16384
 
 typedef enum mad_tensor_kind {
   MAD_TENSOR_AUTO = 0,       /* detect from the level-0 tensor */

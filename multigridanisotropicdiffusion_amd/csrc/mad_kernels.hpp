@@ -886,41 +886,52 @@ __global__ void __launch_bounds__(64) peer_pong_k(const T* mlo, const T* mhi, ui
 // the other GPU are visible), giving up after `tmo` wall-clock ticks with the error word set (a
 // peer that died must not hang this GPU); the last block to finish resets the counters, which no
 // neighbour touches again before this rank's next sweep has signalled it (Solver::peer_resolve).
+// The error word is sticky: once a wait has timed out (here or in an earlier launch) the blocks
+// neither wait nor copy and the counters are left as they are -- a late tile of the neighbour must
+// not release a later batch early -- and the host raises it (Solver::peer_check, called by every
+// entry point that returns results: mad_run, the norms, downloads, mad_synchronize).
 // The mailboxes are uncached, so the copy reads what the neighbour stored; the ghost planes are
 // then ordinary stream-ordered data for the kernels that follow.
 __global__ void __launch_bounds__(256) peer_unpack_k(char* __restrict__ dlo, const char* __restrict__ slo,
                                                      char* __restrict__ dhi, const char* __restrict__ shi,
                                                      uint64_t bytes, uint32_t* __restrict__ ctl, int ci,
                                                      uint32_t tiles, uint64_t tmo) {
+  __shared__ int failed;
   const int side = blockIdx.y;
   char* d = side ? dhi : dlo;
   const char* src = side ? shi : slo;
   if (d) {
     if (threadIdx.x == 0) {
+      int f = __hip_atomic_load(ctl + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
       uint32_t* cnt = ctl + ci + side;
       const uint64_t t0 = wall_clock64();
-      while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < tiles) {
+      while (!f && __hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < tiles) {
         __builtin_amdgcn_s_sleep(2);
         if (wall_clock64() - t0 > tmo) {
           __hip_atomic_store(ctl + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
+          f = 1;
         }
       }
+      failed = f;
     }
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if ((((uintptr_t)d | (uintptr_t)src | bytes) & 15) == 0) {
-      for (uint64_t i = t0; i < bytes / 16; i += stride) ((uint4*)d)[i] = ((const uint4*)src)[i];
-    } else {
-      for (uint64_t i = t0; i < bytes / 4; i += stride) ((uint32_t*)d)[i] = ((const uint32_t*)src)[i];
+    if (!failed) {
+      const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+      const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+      if ((((uintptr_t)d | (uintptr_t)src | bytes) & 15) == 0) {
+        for (uint64_t i = t0; i < bytes / 16; i += stride) ((uint4*)d)[i] = ((const uint4*)src)[i];
+      } else {
+        for (uint64_t i = t0; i < bytes / 4; i += stride) ((uint32_t*)d)[i] = ((const uint32_t*)src)[i];
+      }
     }
   }
   if (threadIdx.x == 0) {
     const uint32_t nb = gridDim.x * gridDim.y;
     if (__hip_atomic_fetch_add(ctl + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) {
-      if (dlo) __hip_atomic_store(ctl + ci, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (dhi) __hip_atomic_store(ctl + ci + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (__hip_atomic_load(ctl + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+        if (dlo) __hip_atomic_store(ctl + ci, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (dhi) __hip_atomic_store(ctl + ci + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       __hip_atomic_store(ctl + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

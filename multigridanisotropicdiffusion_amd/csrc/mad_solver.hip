@@ -1764,6 +1764,7 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipMemcpyAsync(out, dst, N * dtype_size(out_dtype), hipMemcpyDeviceToHost,
                                c_->stream));
     HIP_CHECK(hipStreamSynchronize(c_->stream));
+    peer_check();  // a timed-out peer wait fails the run instead of returning stale halos
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     HIP_CHECK(hipEventDestroy(e0));
@@ -1890,6 +1891,10 @@ class Solver final : public SolverBase {
                                c_->stream));  // MAD.hxx:248-261
     }
     HIP_CHECK(hipEventRecord(e1, c_->stream));
+    // the last folded residual left x holding the last fp32 correction (the zero-iterate sweep
+    // never needed it cleared): leave level-0 x = 0, as the unfolded pass does, for direct
+    // kernel-API use after the run (mad_download, mad_smooth, mad_vcycle)
+    if (refine_emitted_ && zero_sweep_ok()) fill(0, MAD_X, 0.0);
     void* dst = out;
     if (!dev_io) dst = scratch_bytes(N * dtype_size(out_dtype));
     convert_from(u64_, dst, out_dtype, N, c_->stream);  // MAD.hxx:266-289
@@ -1897,6 +1902,7 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipMemcpyAsync(out, dst, N * dtype_size(out_dtype), hipMemcpyDeviceToHost,
                                c_->stream));
     HIP_CHECK(hipStreamSynchronize(c_->stream));
+    peer_check();  // a timed-out peer wait fails the run instead of returning stale halos
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     HIP_CHECK(hipEventDestroy(e0));
@@ -2379,6 +2385,15 @@ class Solver final : public SolverBase {
       REQUIRE(ok, MAD_ERR_SINGULAR, "coarsest operator is singular");
       return;
     }
+    {  // the dense inverse and getrf / getri's copy of A (2 n^2 fp64) must fit on the device
+      const size_t need = 2 * sizeof(double) * (size_t)n * (size_t)n;
+      size_t free_b = 0, total_b = 0;
+      HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      REQUIRE(need < free_b / 10 * 9, MAD_ERR_UNSUPPORTED,
+              "coarsest grid has " + std::to_string(n) + " unknowns: its dense inverse needs " +
+                  std::to_string(need >> 20) + " MiB of device memory, " + std::to_string(free_b >> 20) +
+                  " MiB free (lower mad_desc.coarse_dense_max to use the block-plane LU)");
+    }
     std::vector<double> A((size_t)n * n, 0.0);
     for (int64_t p = 0; p < n; ++p) {
       double* row = &A[(size_t)p * n];
@@ -2647,8 +2662,9 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
-    REQUIRE(d->coarse_dense_max >= 0 && d->coarse_dense_max <= 65536, MAD_ERR_INVALID,
-            "coarse_dense_max must be in [0, 65536]");
+    REQUIRE(d->coarse_dense_max >= 0 && d->coarse_dense_max <= MAD_COARSE_DENSE_LIMIT, MAD_ERR_INVALID,
+            "coarse_dense_max must be in [0, " + std::to_string(MAD_COARSE_DENSE_LIMIT) +
+                "] (a dense inverse of n unknowns takes 8 n^2 bytes on the host and twice that on the device)");
     REQUIRE(d->coarse_block_unknowns >= 0, MAD_ERR_INVALID, "coarse_block_unknowns must be >= 0");
     REQUIRE(d->tensor_kind >= MAD_TENSOR_AUTO && d->tensor_kind <= MAD_TENSOR_FULL,
             MAD_ERR_INVALID, "bad tensor kind");
@@ -2956,13 +2972,14 @@ int mad_smooth(mad_ctx* c, int32_t level, uint32_t sweeps) {
 
 int mad_residual(mad_ctx* c, int32_t level, double* norm_out) {
   KERNEL_ENTRY(CHECK_LEVEL(level); double v = c->solver->residual(level, norm_out != nullptr);
-               if (norm_out) *norm_out = v);
+               if (norm_out) { c->solver->check_device_errors(); *norm_out = v; });
 }
 
 int mad_norm(mad_ctx* c, int32_t level, int32_t which, double* norm_out) {
   KERNEL_ENTRY(CHECK_LEVEL(level); CHECK_WHICH(which);
                REQUIRE(norm_out, MAD_ERR_INVALID, "null output");
-               *norm_out = c->solver->norm(level, which));
+               const double v = c->solver->norm(level, which);
+               c->solver->check_device_errors(); *norm_out = v);
 }
 
 int mad_restrict(mad_ctx* c, int32_t level) {
