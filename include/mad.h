@@ -169,6 +169,11 @@ typedef struct mad_desc {
    launch) -- no exchange after the sweep.  Levels whose sweeps are not fused single launches keep the
    exchange.  Identical results.  Setup-time option (mad_setup maps the windows, collectively). */
 #define MAD_OPT_PEER_HALO 4u
+/* MAD_OPT_COARSE_NO_CHAIN: the block-plane direct solver (mad_coarse.hpp) without its chain
+   matrices KL_i / KU_i even where they fit -- what it does by itself for one-plane blocks whose
+   KL / KU would take more than half the free device memory (e.g. a 512 x 512 x 8 whole-grid
+   solve: 69 instead of 206 GB); one more launch per chain step, the same result to fp64 rounding */
+#define MAD_OPT_COARSE_NO_CHAIN 8u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

@@ -33,6 +33,7 @@ X, B, R = 0, 1, 2
 OPT_EAGER_RANK_VCYCLE = 1
 OPT_OVERLAP_RANK_SWEEP = 2
 OPT_PEER_HALO = 4
+OPT_COARSE_NO_CHAIN = 8
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (

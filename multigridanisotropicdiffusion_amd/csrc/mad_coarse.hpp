@@ -25,7 +25,9 @@
 //                                                then the other rows at once
 //   so the sequential part is 2 (nb - 1) q x q products -- with the chain's matrices
 //   KL_i = Dinv_i[last, first] E_i and KU_i = Dinv_i[first, last] F_i formed at setup,
-//   one GEMV launch per step -- and everything else is bandwidth-parallel.  All arithmetic fp64 (the reference's), deterministic
+//   one GEMV launch per step (blocks of one plane, q >= the block target, whose KL / KU would
+//   not fit next to Dinv, multiply by Dinv_i itself after a sparse E_i y: the same q x q read
+//   without 2 q^2 of extra memory per block) -- and everything else is bandwidth-parallel.  All arithmetic fp64 (the reference's), deterministic
 //   (one wave per row, fixed reduction order): every rank that replicates the
 //   coarsest level computes the same bits.
 #pragma once
@@ -82,20 +84,32 @@ __global__ void __launch_bounds__(256) cs_dinv_k(const double* __restrict__ dinv
   if (lane == 0) cv[r] = s;
 }
 
-// One chain step: cv[row0 + r] -= K[r, :] . cv[src0 .. src0 + q), r < q (K = KL_i or KU_i,
-// q x q row-major); one wave per row.
-__global__ void __launch_bounds__(256) cs_chain_k(const double* __restrict__ K, double* __restrict__ cv, int q,
-                                                  int row0, int src0) {
+// One chain step: cv[row0 + r] -= K[r, :] . v[0 .. q), r < q, K q x q row-major with leading
+// dimension ld -- KL_i / KU_i (ld q, v the neighbour block's plane of cv), or, in the blocks of
+// one plane, Dinv_i itself (ld q, v = E_i y_{i-1} / F_i x_{i+1} from cs_ell_mv_k); one wave per row.
+__global__ void __launch_bounds__(256) cs_chain_k(const double* __restrict__ K, int ld, const double* v,
+                                                  double* cv, int q, int row0) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= q) return;
-  const double* a = K + (size_t)r * q;
-  const double* v = cv + src0;
+  const double* a = K + (size_t)r * ld;
   double s = 0.0;
 #pragma unroll 4
   for (int k = lane; k < q; k += 64) s += a[k] * v[k];
   s = cs_wave_sum(s);
   if (lane == 0) cv[row0 + r] -= s;
+}
+
+// t = E cv[src .. src + q) for one block's coupling E (ELL, q rows x ew): the vector the
+// one-plane blocks' chain step multiplies by Dinv_i (their KL_i = Dinv_i E_i is not stored)
+__global__ void __launch_bounds__(256) cs_ell_mv_k(const int* __restrict__ ec, const double* __restrict__ ev,
+                                                   int ew, const double* __restrict__ src,
+                                                   double* __restrict__ t, int q) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= q) return;
+  double s = 0.0;
+  for (int e = 0; e < ew; ++e) s += ev[(size_t)k * ew + e] * src[ec[(size_t)k * ew + e]];
+  t[k] = s;
 }
 
 // The other rows of every coupled block i = iblk0 + blockIdx.y, after its chain:
@@ -156,21 +170,22 @@ struct CoarseBlocks {
   double* eval = nullptr;
   int* fcol = nullptr;   // F_i ELL (block nb - 1 unused)
   double* fval = nullptr;
-  double* kl = nullptr;  // chain matrices KL_i (q x q per block; block 0 unused)
-  double* ku = nullptr;  // KU_i (block nb - 1 unused)
+  double* kl = nullptr;  // chain matrices KL_i (q x q per block; block 0 unused); only for blocks
+  double* ku = nullptr;  // of > 1 plane -- KU_i (block nb - 1 unused)
   double* bp = nullptr;
   double* cv = nullptr;
+  double* tv = nullptr;  // one-plane blocks: the chain step's coupled vector (q)
   size_t device_bytes = 0;
 
   bool active() const { return dinv != nullptr; }
 
   void release() {
     for (void* p : {(void*)dinv, (void*)perm, (void*)iperm, (void*)ecol, (void*)eval, (void*)fcol,
-                    (void*)fval, (void*)kl, (void*)ku, (void*)bp, (void*)cv})
+                    (void*)fval, (void*)kl, (void*)ku, (void*)bp, (void*)cv, (void*)tv})
       if (p) (void)hipFree(p);
     dinv = nullptr;
     perm = iperm = ecol = fcol = nullptr;
-    eval = fval = kl = ku = bp = cv = nullptr;
+    eval = fval = kl = ku = bp = cv = tv = nullptr;
     n = q = mb = nb = ew = 0;
     device_bytes = 0;
   }
@@ -183,7 +198,7 @@ struct CoarseBlocks {
   }
 
   // bytes this solver would hold on the device for a grid (before building it)
-  static size_t estimate_bytes(int dim, const int64_t nn[3], int target) {
+  static size_t estimate_bytes(int dim, const int64_t nn[3], int target, bool with_chain) {
     int64_t len[3] = {nn[0], nn[1], dim == 3 ? nn[2] : 1};
     const int64_t N = len[0] * len[1] * len[2];
     const int64_t no = std::max({len[0], len[1], len[2]});
@@ -191,15 +206,24 @@ struct CoarseBlocks {
     const int64_t P = planes_per_block((int)q, (int)no, target);
     const int64_t mb = P * q, nb = (no + P - 1) / P;
     const int64_t last = N - (nb - 1) * mb;
-    return (size_t)(((nb - 1) * mb * mb + last * last) * 8 + (2 * nb + 3) * q * q * 8 + N * 160);
+    // Dinv blocks + 3 q^2 of setup workspace (+ 2 nb q^2 of chain matrices)
+    const int64_t chain = with_chain ? 2 * nb : 0;
+    return (size_t)(((nb - 1) * mb * mb + last * last) * 8 + (chain + 3) * q * q * 8 + N * 160);
   }
+  // The chain's KL_i / KU_i (q x q each, formed at setup) make every chain step one GEMV launch.
+  // Without them (build's with_chain false) a step is a sparse E_i y launch and a GEMV over
+  // Dinv_i's q x q corner -- the same bytes, one more launch per step (130 x 130 x 10: 2.93 vs
+  // 2.08 ms per solve), and 2 nb q^2 fewer bytes: blocks of one plane (q >= the block target)
+  // need as much for KL / KU as for Dinv (206 instead of 69 GB at 512 x 512 x 8), so the solver
+  // drops them when they would not fit (Solver::build_coarse_inverse).
+  bool chain_matrices() const { return kl != nullptr; }
 
   using Emit = std::function<void(int64_t col, double val)>;
   using RowFn = std::function<void(int64_t p, const Emit&)>;
 
   // row(p, emit): entries A[p][col] += val of natural row p (any order, duplicates add)
   // returns false if a diagonal block is singular
-  bool build(int dim, const int64_t nn[3], int target, const RowFn& row, hipStream_t stream) {
+  bool build(int dim, const int64_t nn[3], int target, bool with_chain, const RowFn& row, hipStream_t stream) {
     release();
     int64_t len[3] = {nn[0], nn[1], dim == 3 ? nn[2] : 1};
     const int64_t N = len[0] * len[1] * len[2];
@@ -213,8 +237,8 @@ struct CoarseBlocks {
     n = (int)N;
     const int64_t no = len[ax[2]];
     q = (int)(N / no);
-    if (q > 8192) throw std::runtime_error("coarsest grid planes of " + std::to_string(q) +
-                                           " unknowns exceed the direct solver's 8192");
+    // (no bound on q itself: the memory estimate, checked against the device before build, is
+    // the wall -- N q 8 B of Dinv blocks)
     const int P = planes_per_block(q, (int)no, target);
     mb = P * q;
     nb = (int)((no + P - 1) / P);
@@ -294,10 +318,13 @@ struct CoarseBlocks {
     dmalloc((void**)&eval, sizeof(double) * ne);
     dmalloc((void**)&fcol, sizeof(int) * ne);
     dmalloc((void**)&fval, sizeof(double) * ne);
-    dmalloc((void**)&kl, sizeof(double) * nb * q * q);
-    dmalloc((void**)&ku, sizeof(double) * nb * q * q);
+    if (with_chain || mb > q) {  // blocks of > 1 plane: KL / KU are much smaller than Dinv_i
+      dmalloc((void**)&kl, sizeof(double) * nb * q * q);
+      dmalloc((void**)&ku, sizeof(double) * nb * q * q);
+    }
     dmalloc((void**)&bp, sizeof(double) * N);
     dmalloc((void**)&cv, sizeof(double) * N);
+    dmalloc((void**)&tv, sizeof(double) * q);
     auto h2d = [&](void* d, const void* h, size_t bytes) {
       if (hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
         throw std::runtime_error("direct solver: upload failed");
@@ -373,6 +400,7 @@ struct CoarseBlocks {
             rocsolver_dgetri(h, m, Di, m, ipiv, info + 2 * i + 1) != rocblas_status_success)
           throw std::runtime_error("rocsolver getrf/getri failed");
         // chain matrices: KL_i = Dinv_i[last, first] E_i, KU_i = Dinv_i[first, last] F_i
+        if (!chain_matrices()) continue;
         if (i > 0)  // dE still holds E_i (the Schur update above)
           rm_gemm(q, q, q, 1.0, Di + (size_t)(m - q) * m, m, dE, q, 0.0, kl + (size_t)i * q * q, q);
         if (i < nb - 1) {
@@ -408,17 +436,32 @@ struct CoarseBlocks {
     const size_t lds = sizeof(double) * q;
     const unsigned gc = (unsigned)((q + 3) / 4);
     const unsigned gr = (unsigned)((mb - q + 31) / 32);
+    const bool km = chain_matrices();  // else one plane per block (mb == q)
+    const unsigned ge = (unsigned)((q + 255) / 256);
     for (int i = 1; i < nb; ++i) {  // y_i[last] = c_i[last] - KL_i y_{i-1}[last]
       const int r0 = i * mb, m = std::min(mb, n - r0);
-      hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, kl + (size_t)i * q * q, cv, q, r0 + m - q,
-                         r0 - q);
+      if (km) {
+        hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, kl + (size_t)i * q * q, q, cv + (r0 - q), cv,
+                           q, r0 + m - q);
+      } else {  // one plane per block: KL_i y = Dinv_i (E_i y)
+        hipLaunchKernelGGL(cs_ell_mv_k, dim3(ge), b256, 0, stream, ecol + (size_t)i * q * ew,
+                           eval + (size_t)i * q * ew, ew, cv + (r0 - q), tv, q);
+        hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, dinv + (size_t)i * mb * mb, q, tv, cv, q, r0);
+      }
     }
     if (mb > q && nb > 1)
       hipLaunchKernelGGL((cs_couple_k<false>), dim3(gr, (unsigned)(nb - 1)), b256, lds, stream, dinv, ecol, eval,
                          ew, cv, n, mb, q, 1);
-    for (int i = nb - 2; i >= 0; --i)  // x_i[first] = y_i[first] - KU_i x_{i+1}[first]
-      hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, ku + (size_t)i * q * q, cv, q, i * mb,
-                         (i + 1) * mb);
+    for (int i = nb - 2; i >= 0; --i) {  // x_i[first] = y_i[first] - KU_i x_{i+1}[first]
+      if (km) {
+        hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, ku + (size_t)i * q * q, q, cv + (i + 1) * mb,
+                           cv, q, i * mb);
+      } else {  // KU_i x = Dinv_i (F_i x)
+        hipLaunchKernelGGL(cs_ell_mv_k, dim3(ge), b256, 0, stream, fcol + (size_t)i * q * ew,
+                           fval + (size_t)i * q * ew, ew, cv + (i + 1) * mb, tv, q);
+        hipLaunchKernelGGL(cs_chain_k, dim3(gc), b256, 0, stream, dinv + (size_t)i * mb * mb, q, tv, cv, q, i * mb);
+      }
+    }
     if (mb > q && nb > 1)
       hipLaunchKernelGGL((cs_couple_k<true>), dim3(gr, (unsigned)(nb - 1)), b256, lds, stream, dinv, fcol, fval,
                          ew, cv, n, mb, q, 0);

@@ -832,49 +832,65 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   }
 }
 
-// Peer halo self-test at setup (Solver::peer_selftest): each edge writes a token into the
-// neighbour's mailbox with the sweep's store / completion / counter pattern (peer_ping_k), then
-// every rank checks that both neighbours' tokens and counts arrived (peer_pong_k, bounded wait),
-// resets its counters and reports -- so a cross-GPU path that does not deliver is found before
-// the first sweep, and the ranks fall back to the exchange together.
+// Peer halo self-test at setup (Solver::peer_selftest): every edge fills the WHOLE neighbour
+// mailbox it will write (GHOST planes, ghost_n elements) with a pattern of the sending rank,
+// through the sweep's own store path -- buffer stores with an SGPR base and per-lane offsets,
+// s_waitcnt 0 before a barrier, then one relaxed system-scope counter increment per workgroup
+// (peer_ping_k) -- and every receiver waits for all its neighbours' workgroups (bounded) and
+// checks every element of both mailboxes (peer_pong_k); a missing count or a single wrong value
+// makes every rank fall back to the exchange for that level.  blockIdx.y = side.
+__device__ __forceinline__ uint32_t peer_pattern(int rank, int64_t e) {
+  return (uint32_t)(rank + 1) * 1021u + (uint32_t)(e % 4093);  // < 2^24: exact in fp32 too
+}
 template <typename T>
-__global__ void __launch_bounds__(64) peer_ping_k(PeerOut<T> po, T token) {
-  T* d = po.dst[blockIdx.x];
+__global__ void __launch_bounds__(256) peer_ping_k(PeerOut<T> po, int64_t ghost_n, int64_t top_off, int rank) {
+  const int side = blockIdx.y;
+  T* d = po.dst[side];
   if (!d) return;
-  d[threadIdx.x] = token;
+  T* base = d - (side ? top_off : 0);  // the top edge's pointer is at its mailbox's last plane
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e0 = (int64_t)blockIdx.x * 256; e0 < ghost_n; e0 += stride) {
+    const int64_t e = e0 + threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(base + e0);
+    if (e < ghost_n) buf_store<T>((T)peer_pattern(rank, e), r, threadIdx.x * (uint32_t)sizeof(T));
+  }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(po.sig[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(po.sig[side], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// okw (plain device memory, 1 before the launch) is cleared on any failure; the counters are
+// reset by the host afterwards (nothing writes them again before the collective that follows)
 template <typename T>
-__global__ void __launch_bounds__(64) peer_pong_k(const T* mlo, const T* mhi, uint32_t* clo, uint32_t* chi,
-                                                  T tlo, T thi, uint32_t* okw, uint64_t tmo) {
-  __shared__ int good;
+__global__ void __launch_bounds__(256) peer_pong_k(const T* mlo, const T* mhi, const uint32_t* clo,
+                                                   const uint32_t* chi, int rlo, int rhi, int64_t ghost_n,
+                                                   uint32_t expect, uint32_t* okw, uint64_t tmo) {
+  __shared__ int arrived;
+  const int side = blockIdx.y;
+  const T* m = side ? mhi : mlo;
+  const uint32_t* cnt = side ? chi : clo;
+  const int sender = side ? rhi : rlo;
+  if (!m) return;
   if (threadIdx.x == 0) {
-    good = 1;
-    uint32_t* cs[2] = {clo, chi};
-    for (int q = 0; q < 2; ++q) {
-      if (!cs[q]) continue;
-      const uint64_t t0 = wall_clock64();
-      while (__hip_atomic_load(cs[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < 1u) {
-        __builtin_amdgcn_s_sleep(2);
-        if (wall_clock64() - t0 > tmo) {
-          good = 0;
-          break;
-        }
+    int ok = 1;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < expect) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > tmo) {
+        ok = 0;
+        break;
       }
     }
+    arrived = ok;
   }
   __syncthreads();
-  const bool bad = (mlo && mlo[threadIdx.x] != tlo) || (mhi && mhi[threadIdx.x] != thi);
-  if (bad) atomicAnd(&good, 0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (clo) __hip_atomic_store(clo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (chi) __hip_atomic_store(chi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(okw, (uint32_t)good, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool bad = !arrived;
+  if (arrived) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < ghost_n; e += stride)
+      bad |= m[e] != (T)peer_pattern(sender, e);
   }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) atomicAnd(okw, 0u);
 }
 
 // Peer halo, consumer side: wait for the neighbours' edge planes, copy the two mailboxes into

@@ -501,28 +501,33 @@ class Solver final : public SolverBase {
       L.peer = true;
     }
   }
-  // one token per edge through the mapped windows, checked on every rank (collective)
+  // every mailbox filled through the mapped windows with the sending rank's pattern by the
+  // sweep's store / completion / counter pattern, every element checked on the receiving rank
+  // (collective; peer_ping_k / peer_pong_k)
   bool peer_selftest(LevelData<T>& L) {
     const int r = c_->comm.rank();
     const bool self = c_->comm.stand_in();
-    auto token = [](int rank) { return T(1000) * T(rank + 1) + T(7); };
-    hipLaunchKernelGGL((peer_ping_k<T>), dim3(2), dim3(64), 0, c_->stream, peer_out(L, 0), token(r));
+    const int64_t n = (int64_t)L.ghost;
+    const int64_t top = (int64_t)(GHOST - 1) * L.g.sz;
+    const unsigned nblk = (unsigned)std::min<int64_t>(256, std::max<int64_t>(1, (n + 255) / 256));
+    uint32_t* ctl = peer_ctl(L.win, L);
+    const uint32_t one = 1u;
+    HIP_CHECK(hipMemcpyAsync(ctl + 6, &one, sizeof one, hipMemcpyHostToDevice, c_->stream));
+    // every rank's ok word is set before any neighbour's ping can count in
+    c_->comm.local_barrier(c_->stream);
+    hipLaunchKernelGGL((peer_ping_k<T>), dim3(nblk, 2), dim3(256), 0, c_->stream, peer_out(L, 0), n, top, r);
     HIP_CHECK(hipGetLastError());
     // the in-process transport's ranks share one device's hardware queues: all pings done first
     c_->comm.local_barrier(c_->stream);
-    const int64_t top = (int64_t)(GHOST - 1) * L.g.sz;
-    const T* mlo = nullptr;
-    const T* mhi = nullptr;
-    if (L.g.zlo_ghost) mlo = mailbox(L.win, L, 0, 0) + (self ? 0 : top);
-    if (L.g.zhi_ghost) mhi = mailbox(L.win, L, 0, 1) + (self ? top : 0);
-    uint32_t* ctl = peer_ctl(L.win, L);
+    const T* mlo = L.g.zlo_ghost ? mailbox(L.win, L, 0, 0) : nullptr;
+    const T* mhi = L.g.zhi_ghost ? mailbox(L.win, L, 0, 1) : nullptr;
     const uint64_t tmo = peer_timeout_ticks_ / 10;  // 2 s
-    hipLaunchKernelGGL((peer_pong_k<T>), dim3(1), dim3(64), 0, c_->stream, mlo, mhi,
-                       L.g.zlo_ghost ? ctl + 0 : nullptr, L.g.zhi_ghost ? ctl + 1 : nullptr,
-                       token(self ? r : r - 1), token(self ? r : r + 1), ctl + 6, tmo);
+    hipLaunchKernelGGL((peer_pong_k<T>), dim3(nblk, 2), dim3(256), 0, c_->stream, mlo, mhi, ctl + 0, ctl + 1,
+                       self ? r : r - 1, self ? r : r + 1, n, nblk, ctl + 6, tmo);
     HIP_CHECK(hipGetLastError());
     uint32_t ok = 0;
     HIP_CHECK(hipMemcpyAsync(&ok, ctl + 6, sizeof ok, hipMemcpyDeviceToHost, c_->stream));
+    HIP_CHECK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), c_->stream));  // counters of buffer 0
     HIP_CHECK(hipStreamSynchronize(c_->stream));
     return c_->comm.all_true(ok == 1u, c_->stream);
   }
@@ -2366,9 +2371,16 @@ class Solver final : public SolverBase {
     const int64_t dense_max = c_->d.coarse_dense_max > 0 ? c_->d.coarse_dense_max : MAD_COARSE_DENSE_MAX;
     const int target = c_->d.coarse_block_unknowns > 0 ? c_->d.coarse_block_unknowns : MAD_COARSE_BLOCK_UNKNOWNS;
     if (n > dense_max) {
-      const size_t need = CoarseBlocks::estimate_bytes(dim, G.n, target);
       size_t free_b = 0, total_b = 0;
       HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      // KL / KU chain matrices where they take at most half the free memory (one launch per
+      // chain step); without them down to the Dinv blocks alone
+      // (every rank that replicates the level takes the same decision: the same bits per solve)
+      const bool with_chain = c_->comm.all_true(
+          CoarseBlocks::estimate_bytes(dim, G.n, target, true) < free_b / 2 &&
+              !(c_->d.options & MAD_OPT_COARSE_NO_CHAIN),
+          c_->stream);
+      const size_t need = CoarseBlocks::estimate_bytes(dim, G.n, target, with_chain);
       REQUIRE(need < free_b / 10 * 9, MAD_ERR_UNSUPPORTED,
               "coarsest grid has " + std::to_string(n) + " unknowns: its direct solver needs " +
                   std::to_string(need >> 20) + " MiB of device memory, " + std::to_string(free_b >> 20) +
@@ -2376,7 +2388,7 @@ class Solver final : public SolverBase {
                   "GH.hxx:36-59)");
       bool ok = false;
       try {
-        ok = cblk_.build(dim, G.n, target,
+        ok = cblk_.build(dim, G.n, target, with_chain,
                          [&](int64_t p, const CoarseBlocks::Emit& emit) { coarse_row(p, emit); },
                          c_->stream);
       } catch (const std::runtime_error& e) {
@@ -2658,7 +2670,8 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             "bad rank / nranks");
     REQUIRE(d->gs_kernel == 0 || d->gs_kernel == 1 || d->gs_kernel == 3 || d->gs_kernel == 4,
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
-    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO)) == 0,
+    REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO |
+                            MAD_OPT_COARSE_NO_CHAIN)) == 0,
             MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
