@@ -687,6 +687,12 @@ class Solver final : public SolverBase {
     // needs a large slab to fill the chip; below ~4M voxels one launch per colour is
     // faster (measured: 256^3 fused 0.23 ms vs 0.28 ms, 128^3 fused 0.13 vs 0.064 ms)
     const Geo& g = lv_[l].g;
+#ifndef MAD_FUSED_RANK_MIN_VOXELS  // rank slabs (A/B knob, tools/rank_fused_ab.sh)
+#define MAD_FUSED_RANK_MIN_VOXELS ((int64_t)4 << 20)
+#define MAD_FUSED_RANK_MIN_PLANES 64
+#endif
+    if (c_->geom[l].distributed)
+      return (int64_t)g.nx * g.ny * g.nz >= (int64_t)MAD_FUSED_RANK_MIN_VOXELS && g.nz >= MAD_FUSED_RANK_MIN_PLANES;
     return (int64_t)g.nx * g.ny * g.nz >= (int64_t)4 << 20 && g.nz >= 64;
   }
 
