@@ -33,6 +33,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
+
+#include "mad_alloc.hpp"
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
@@ -306,7 +308,7 @@ struct CoarseBlocks {
     const int64_t last = N - (int64_t)(nb - 1) * mb;
     const size_t dinv_elems = (size_t)(nb - 1) * mb * mb + (size_t)last * last;
     auto dmalloc = [&](void** ptr, size_t bytes) {
-      if (hipMalloc(ptr, bytes) != hipSuccess)
+      if (big_alloc(ptr, bytes) != hipSuccess)
         throw std::runtime_error("direct solver: device allocation of " + std::to_string(bytes) + " B failed");
       device_bytes += bytes;
     };

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/mad.h"
+#include "mad_alloc.hpp"
 #include "mad_coarse.hpp"
 #include "mad_comm.hpp"
 #include "mad_kernels.hpp"
@@ -353,7 +354,7 @@ class Solver final : public SolverBase {
       const int64_t margin = margin_elems(L.g);
       const int64_t tot = L.g.N + 2 * (L.ghost + margin);
       for (int a = 0; a < 4; ++a) {
-        HIP_CHECK(hipMalloc(&L.alloc[a], sizeof(T) * tot));
+        level_alloc((void**)&L.alloc[a], sizeof(T) * tot);
         HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
       }
       L.x = L.alloc[0] + margin + L.ghost;
@@ -379,7 +380,7 @@ class Solver final : public SolverBase {
       const int64_t cgp = (dim == 3) ? GHOST : 0;
       const int64_t cmargin = margin * L.g.rs;
       const int64_t ctot = (L.g.nz + 2 * cgp) * cplane + 2 * cmargin;
-      HIP_CHECK(hipMalloc(&L.cf_alloc, sizeof(T) * ctot));
+      level_alloc((void**)&L.cf_alloc, sizeof(T) * ctot);
       HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
@@ -391,7 +392,7 @@ class Solver final : public SolverBase {
       const int64_t margin = margin_elems(L0.g);
       const int64_t tot = L0.g.N + 2 * (L0.ghost + margin);
       for (auto& a : r64alloc_) {
-        HIP_CHECK(hipMalloc(&a, sizeof(double) * tot));
+        HIP_CHECK(big_alloc((void**)&a, sizeof(double) * tot));
         HIP_CHECK(hipMemsetAsync(a, 0, sizeof(double) * tot, c->stream));
       }
       u64_ = r64alloc_[0] + margin + L0.ghost;
@@ -400,7 +401,7 @@ class Solver final : public SolverBase {
       const int64_t cgp = (dim == 3) ? GHOST : 0;
       const int64_t cplane = L0.g.sz * ncoef_;
       const int64_t ctot = (L0.g.nz + 2 * cgp) * cplane + 2 * margin * ncoef_;
-      HIP_CHECK(hipMalloc(&cf64_alloc_, sizeof(double) * ctot));
+      HIP_CHECK(big_alloc((void**)&cf64_alloc_, sizeof(double) * ctot));
       HIP_CHECK(hipMemsetAsync(cf64_alloc_, 0, sizeof(double) * ctot, c->stream));
       cf64_ = cf64_alloc_ + margin * ncoef_ + cgp * cplane;
       for (int d = 0; d < 3; ++d) rat64_.r[d] = (c->geom[0].h[0] * c->geom[0].h[0]) / (c->geom[0].h[d] * c->geom[0].h[d]);
@@ -437,6 +438,9 @@ class Solver final : public SolverBase {
     setup_peer();
     HIP_CHECK(hipStreamSynchronize(c->stream));
   }
+
+  // level arrays (x, b, r, t, coefficient records): mad_alloc.hpp
+  static void level_alloc(void** p, size_t bytes) { HIP_CHECK(contiguous_alloc(p, bytes)); }
 
   // ------------------------------------------------------------- peer halo
   // MAD_OPT_PEER_HALO: on every distributed level whose sweeps are fused single launches with
@@ -2110,7 +2114,7 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipStreamSynchronize(c_->stream));
       if (scratch_) HIP_CHECK(hipFree(scratch_));
       scratch_ = nullptr;
-      HIP_CHECK(hipMalloc(&scratch_, bytes));
+      HIP_CHECK(big_alloc((void**)&scratch_, bytes));
       scratch_cap_ = bytes;
     }
     return scratch_;
@@ -2293,7 +2297,7 @@ class Solver final : public SolverBase {
     const LevelGeom& G = c_->geom[c_->nlev - 1];
     const int nc = coef_count(dim, c_->kind);
     double* cf64 = nullptr;
-    HIP_CHECK(hipMalloc(&cf64, sizeof(double) * G.N * nc));
+    HIP_CHECK(big_alloc((void**)&cf64, sizeof(double) * G.N * nc));
     dim3 gr = grid_for((int)G.n[0], (int)G.n[1], (int)G.n[2], BLK);
     dispatch(dim, c_->kind, [&](auto D, auto K) {
       hipLaunchKernelGGL((build_coef_k<double, D.value, K.value>), gr, BLK, 0, c_->stream,
@@ -2537,7 +2541,7 @@ double* tensor_at0(const mad_ctx* c) {
 void tensor_alloc(mad_ctx* c) {
   if (c->tensor64) return;
   const int ncomp = c->dim * (c->dim + 1) / 2;
-  HIP_CHECK(hipMalloc(&c->tensor64, sizeof(double) * ncomp * c->tensor_cs));
+  HIP_CHECK(big_alloc((void**)&c->tensor64, sizeof(double) * ncomp * c->tensor_cs));
   // ghost planes outside the grid stay zero (never read)
   if (c->tensor_tg) HIP_CHECK(hipMemsetAsync(c->tensor64, 0, sizeof(double) * ncomp * c->tensor_cs, c->stream));
 }

@@ -233,7 +233,7 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
   REQUIRE(nx >= 4 && ny >= 4 && nz >= 4, MAD_ERR_UNSUPPORTED,
           "the recursive Gaussian needs at least 4 points along each axis");
   const int64_t N = v->N;
-  if (!v->iir) HIP_CHECK(hipMalloc(&v->iir, sizeof(double) * 12 * N));
+  if (!v->iir) HIP_CHECK(big_alloc((void**)&v->iir, sizeof(double) * 12 * N));
   // volumes between the passes in T: fp64 in the fp64 mode; fp32 in the fp32 mode (the
   // passes' arithmetic stays fp64; half the bytes of the memory-bound passes)
   T* base = reinterpret_cast<T*>(v->iir);
@@ -344,7 +344,7 @@ void ved_scale_iir(mad_ved_ctx* v, double sigma, int mode, bool first, double* h
     if (tot > v->xbuf_bytes) {
       if (v->xbuf) HIP_CHECK(hipFree(v->xbuf));
       v->xbuf = nullptr;
-      HIP_CHECK(hipMalloc(&v->xbuf, tot));
+      HIP_CHECK(big_alloc((void**)&v->xbuf, tot));
       v->xbuf_bytes = tot;
     }
     Vol6<T> Z3{};
@@ -427,7 +427,7 @@ void ved_scale(mad_ved_ctx* v, double sigma, int mode, bool first, double* hess,
   hipStream_t st = v->mad->stream;
   const int nx = (int)v->n[0], ny = (int)v->n[1], nz = (int)v->n[2];
   const int64_t N = v->N;
-  if (!v->fir) HIP_CHECK(hipMalloc(&v->fir, sizeof(T) * 9 * N));
+  if (!v->fir) HIP_CHECK(big_alloc((void**)&v->fir, sizeof(T) * 9 * N));
   T* f = (T*)v->fir;
   T *z0 = f, *z1 = f + N, *z2 = f + 2 * N;
   T *a00 = f + 3 * N, *a10 = f + 4 * N, *a20 = f + 5 * N, *a01 = f + 6 * N, *a11 = f + 7 * N,
@@ -484,8 +484,8 @@ template <typename T>
 void ved_tensor_impl(mad_ved_ctx* v) {
   mad_ctx* c = v->mad;
   const int64_t N = v->N;
-  if (!v->resp) HIP_CHECK(hipMalloc(&v->resp, sizeof(double) * N));
-  if (!v->dir) HIP_CHECK(hipMalloc(&v->dir, sizeof(double) * 3 * N));
+  if (!v->resp) HIP_CHECK(big_alloc((void**)&v->resp, sizeof(double) * N));
+  if (!v->dir) HIP_CHECK(big_alloc((void**)&v->dir, sizeof(double) * 3 * N));
   // the run's tensor: partitioned across the ranks (recursive Hessian; the FIR operator and
   // the line-walk reference stay whole-grid on every rank)
   for (int s = 0; s < v->d.nscales; ++s) ved_scale<T>(v, v->d.scales[s], VED_UPDATE, s == 0, nullptr, true);
@@ -650,8 +650,8 @@ int mad_ved_create(const mad_ved_desc* d, mad_ved_ctx** out) {
     REQUIRE(v->n[0] <= INT32_MAX && v->n[1] <= 65535 && v->n[2] <= 65535, MAD_ERR_INVALID,
             "image too large for the VED grid mapping");
     HIP_CHECK(hipSetDevice(v->mad->device));
-    HIP_CHECK(hipMalloc(&v->img, sizeof(double) * v->N));
-    HIP_CHECK(hipMalloc(&v->img2, sizeof(double) * v->N));
+    HIP_CHECK(big_alloc((void**)&v->img, sizeof(double) * v->N));
+    HIP_CHECK(big_alloc((void**)&v->img2, sizeof(double) * v->N));
   });
   if (rc != MAD_OK) return rc;
   *out = v.release();
@@ -729,7 +729,7 @@ int mad_ved_hessian(mad_ved_ctx* v, const void* image, int32_t dtype, double sig
     HIP_CHECK(hipSetDevice(v->mad->device));
     ved_load_image(v, image, dtype, false);
     double* H = nullptr;
-    HIP_CHECK(hipMalloc(&H, sizeof(double) * 6 * v->N));
+    HIP_CHECK(big_alloc((void**)&H, sizeof(double) * 6 * v->N));
     if (v->d.precision == MAD_FP64) ved_scale<double>(v, sigma, VED_HESSIAN, true, H);
     else ved_scale<float>(v, sigma, VED_HESSIAN, true, H);
     HIP_CHECK(hipMemcpyAsync(hessian_soa, H, sizeof(double) * 6 * v->N, hipMemcpyDeviceToHost,
