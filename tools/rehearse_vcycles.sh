@@ -7,4 +7,4 @@ tr 29624 --options 4
 echo "== bench rehearsal rccl"
 MAD_BENCH_SHARED_GPU=1 timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29625 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --no-precision-cycles --halo rccl 2>&1 | grep -E "bench rank|metric|WARN|Error"; echo "rc=$?"
 echo "== bench rehearsal peer"
-MAD_BENCH_SHARED_GPU=1 timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29626 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --no-precision-cycles 2>&1 | grep -E "bench rank|metric|WARN|Error"; echo "rc=$?"
+MAD_BENCH_SHARED_GPU=1 timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29626 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --no-precision-cycles --halo peer 2>&1 | grep -E "bench rank|metric|WARN|Error"; echo "rc=$?"
