@@ -78,6 +78,10 @@ typedef enum mad_precision {
   MAD_FP32 = 0, MAD_FP64 = 1, MAD_FP32_REFINE = 2, MAD_PRECISION_AUTO = 3
 } mad_precision;
 #define MAD_FP32_TOLERANCE_FLOOR 1e-6
+/* MAD_FP32_REFINE V-cycle / FMG solves run their first cycles in plain fp32 (fp32 iterate, fp32
+   residual norm) until relres drops below this, far above fp32's ~1e-7 floor; the iterate then moves
+   to fp64 and the defect correction continues (SMOOTHER runs refine from the first sweep) */
+#define MAD_REFINE_SWITCH_RELRES 1e-5
 /* defaults of mad_desc.min_slab_planes / min_slab_voxels (measured: profiles/r03_agglomeration.md,
    profiles/r03_rank_serial_ab.md) */
 #define MAD_MIN_SLAB_PLANES 4

@@ -1843,12 +1843,25 @@ class Solver final : public SolverBase {
     for (unsigned step = 0; step < d.number_of_steps; ++step) {  // MAD.hxx:158
       if (d.verbose && d.number_of_steps > 1 && c_->comm.rank() == 0)
         std::printf("\n------------ Time step n. %u / %u------------\n", step + 1, d.number_of_steps);
+      // V-cycle / FMG solves start in plain fp32 (the fp32 iterate on the fp32 rhs, fp32 residual
+      // norms) while relres is far above fp32's floor: those cycles reduce the error as the refined
+      // ones would, at the fp32 cycle's cost; below MAD_REFINE_SWITCH_RELRES the iterate moves to
+      // fp64 and the defect correction takes over (SMOOTHER runs refine from the first sweep: their
+      // unconverged output depends on every sweep's rounding)
+      const bool fp32_phase = d.cycle != MAD_SMOOTHER;
       if (d.cycle == MAD_FMG) {
         if (d.verbose && c_->comm.rank() == 0) std::printf("|--- Full Multigrid Cycle ---|\n");
         to_fp32_rhs(b64_);
         fmg_rec(0);  // MAD.hxx:170-176, in fp32
-        hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, c_->stream, L0.x, u64_, N);
-        HIP_CHECK(hipGetLastError());
+        if (!fp32_phase) {
+          hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, c_->stream, L0.x, u64_, N);
+          HIP_CHECK(hipGetLastError());
+        }
+      } else if (fp32_phase) {
+        to_fp32_rhs(b64_);
+        HIP_CHECK(hipMemcpyAsync(L0.x, L0.b, sizeof(T) * N, hipMemcpyDeviceToDevice,
+                                 c_->stream));  // MAD.hxx:177-201
+        x_changed(0);
       } else {
         HIP_CHECK(hipMemcpyAsync(u64_, b64_, sizeof(double) * N, hipMemcpyDeviceToDevice,
                                  c_->stream));  // MAD.hxx:177-201
@@ -1856,14 +1869,36 @@ class Solver final : public SolverBase {
       const double rhsNorm = norm64(b64_);  // MAD.hxx:204
       REQUIRE(std::isfinite(rhsNorm), MAD_ERR_NUMERIC,
               "non-finite right-hand side norm (NaN/Inf in the input image)");
-      double resNorm = residual64();
-      REQUIRE(std::isfinite(resNorm), MAD_ERR_NUMERIC,
-              "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
       unsigned it = 0;
       std::vector<double> hist;
       const unsigned window = (d.cycle == MAD_SMOOTHER) ? 50 : 5;
       bool stalled = false;
-      do {  // MAD.hxx:207-246
+      if (fp32_phase) {
+        do {  // MAD.hxx:207-246 in fp32
+          if (d.verbose && c_->comm.rank() == 0) std::printf("\n|--- VCycle n. %u ---|\n", it + 1);
+          vcycle_fast();
+          const double rn = residual_impl(0, true, false);
+          REQUIRE(std::isfinite(rn), MAD_ERR_NUMERIC,
+                  "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
+          relres = (rhsNorm > 0.0) ? rn / rhsNorm : rn;
+          ++it;
+          trace(step, relres);
+          hist.push_back(relres);
+        } while (relres > std::max(d.tolerance, MAD_REFINE_SWITCH_RELRES) && it < d.max_cycles);
+        hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, c_->stream, L0.x, u64_, N);
+        HIP_CHECK(hipGetLastError());
+      }
+      double resNorm = residual64();
+      REQUIRE(std::isfinite(resNorm), MAD_ERR_NUMERIC,
+              "non-finite residual norm (NaN/Inf in the tensor or the iterate)");
+      if (fp32_phase) {  // the switch iterate's relres, now from the fp64 residual
+        relres = (rhsNorm > 0.0) ? resNorm / rhsNorm : resNorm;
+        if (!hist.empty()) {
+          hist.back() = relres;
+          c_->trace.back().relres = relres;
+        }
+      }
+      if (!fp32_phase || (relres > d.tolerance && it < d.max_cycles)) do {  // MAD.hxx:207-246
         if (refine_emitted_) {  // b = (T) r and x = 0 written by residual64's pass
           L0.b_halo_ok = L0.brec_ok = false;
           x_changed(0);
