@@ -1848,7 +1848,11 @@ class Solver final : public SolverBase {
       // ones would, at the fp32 cycle's cost; below MAD_REFINE_SWITCH_RELRES the iterate moves to
       // fp64 and the defect correction takes over (SMOOTHER runs refine from the first sweep: their
       // unconverged output depends on every sweep's rounding)
+#ifdef MAD_NO_REFINE_FP32_PHASE  // A/B: refine from the first cycle
+      const bool fp32_phase = false;
+#else
       const bool fp32_phase = d.cycle != MAD_SMOOTHER;
+#endif
       if (d.cycle == MAD_FMG) {
         if (d.verbose && c_->comm.rank() == 0) std::printf("|--- Full Multigrid Cycle ---|\n");
         to_fp32_rhs(b64_);
