@@ -52,12 +52,12 @@ def parse():
                    help="(internal) print cpu_baseline(--cpu-seconds, --cpu-size) as JSON and exit")
     p.add_argument("--cpu-timeout", type=float, default=300.0,
                    help="bound of the CPU leg at the benched size (then the 128^3 fallback)")
-    p.add_argument("--halo", default="rccl", choices=["peer", "rccl"],
-                   help="rank slabs (N > 1): 'rccl' (default) -- a grouped ncclSend / ncclRecv "
-                        "exchange after each sweep; 'peer' -- the fused level-0 sweep stores its edge "
-                        "planes into the neighbours' mailboxes while it runs (MAD_OPT_PEER_HALO; not the "
-                        "default until a one-process-per-GPU run has shown it bitwise equal to the "
-                        "in-process transport, tests/test_gpu_multiproc.py)")
+    p.add_argument("--halo", default="auto", choices=["auto", "peer", "rccl"],
+                   help="rank slabs (N > 1): 'rccl' -- a grouped ncclSend / ncclRecv exchange after "
+                        "each sweep; 'peer' -- the fused level-0 sweep stores its edge planes into the "
+                        "neighbours' mailboxes while it runs (MAD_OPT_PEER_HALO); 'auto' (default) -- "
+                        "peer, but only after this run has checked on every rank that it gives the "
+                        "same bits as the rccl exchange (verify_peer), else rccl")
     return p.parse_args()
 
 
@@ -275,6 +275,37 @@ def load_traffic(tag, kernel_sig):
 T0 = time.perf_counter()
 
 
+def verify_peer(M, s, make, rank, sweeps=4):
+    """--halo auto: the peer-halo solver `s` and a second solver exchanging through RCCL sweep
+    the same synthetic system `sweeps` times (both mailbox buffers twice) and every rank compares
+    its slab bit for bit; the peer halo is used only if all ranks agree.  Collective: every rank
+    reaches the same allreduce whatever its own outcome.  Leaves `s` at the initial x again.
+    Returns (ok, note)."""
+    import numpy as np
+    phase(rank, f"halo auto: {sweeps} peer sweeps vs {sweeps} rccl sweeps, bitwise")
+    err = None
+    try:
+        s.smooth(0, sweeps)
+        xp = s.download(0, M.capi.X)
+    except Exception as e:  # a timed-out mailbox wait (peer_check) or any device error
+        err, xp = f"{type(e).__name__}: {e}"[:200], None
+    ref = make(M.SMOOTHER, 0, "halo-check")
+    ref.smooth(0, sweeps)
+    xr = ref.download(0, M.capi.X)
+    same = xp is not None and xp.shape == xr.shape and np.array_equal(xp.view(np.uint32), xr.view(np.uint32))
+    agree = float(ref.allreduce([0.0 if same else 1.0], "max")[0]) == 0.0
+    ref.close()
+    if agree:
+        s.synth_level(0, M.capi.X, 3)
+        s.synchronize()
+        return True, (f"verified in this run: {sweeps} sweeps bitwise equal to the rccl exchange on "
+                      "every rank")
+    if err:
+        return False, f"rank {rank}: {err}"
+    return False, ("this rank's slab differed from the rccl exchange" if not same
+                   else "another rank's slab differed from the rccl exchange, or its peer sweeps failed")
+
+
 def phase(rank, what):
     """One progress line per phase on stderr (the JSON line alone goes to stdout): a run that
     stops shows where, on every rank."""
@@ -315,23 +346,42 @@ def main():
     nz_local = S // world
     shape = (nz_local, S, S)
     sm = M.GAUSS_SEIDEL if a.smoother == "gs" else M.WEIGHTED_JACOBI
-    opts = M.capi.OPT_PEER_HALO if (world > 1 and a.halo == "peer") else 0
+
+    def make(cycle, opts, tag):
+        """A rank's solver of the 512^3 volume, set up with the synthetic tensor, b and x."""
+        sv = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
+                      cycle=cycle, nranks=world, rank=rank, device=local if world > 1 else -1,
+                      global_shape=gshape, gs_kernel=a.gs_kernel, options=opts)
+        if world > 1:
+            phase(rank, f"{tag} solver: joining the communicator")
+            MD.bootstrap_node(sv, rank, world, tag=tag)
+        phase(rank, f"{tag} solver: setup")
+        sv.synth_tensor(kind=0, seed=4)
+        sv.setup()
+        sv.synth_level(0, M.capi.B, 3)
+        sv.synth_level(0, M.capi.X, 3)
+        sv.synchronize()
+        return sv
+
     # SMOOTHER mode (the reference's CycleType 2: repeated sweeps of one system) -- the
     # smoother-only protocol of SURVEY §8(d); level-0 records then carry b (mad_solver.hip)
-    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
-                 cycle=M.SMOOTHER,
-                 nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
-                 gs_kernel=a.gs_kernel, options=opts)
-    if world > 1:
-        phase(rank, "sweep solver: joining the communicator")
-        MD.bootstrap_node(s, rank, world, tag="sweep")
-    phase(rank, "sweep solver: setup")
-    s.synth_tensor(kind=0, seed=4)
-    s.setup()
-    s.synth_level(0, M.capi.B, 3)
-    s.synth_level(0, M.capi.X, 3)
-    s.synchronize()
-
+    want_peer = world > 1 and a.halo in ("auto", "peer")
+    opts = M.capi.OPT_PEER_HALO if want_peer else 0
+    s = make(M.SMOOTHER, opts, "sweep")
+    halo_note = None
+    if want_peer:
+        if "peer halo" not in s.smooth_kernel_name(0):
+            halo_note = "peer halo requested, not engaged at setup (window mapping or self-test): rccl"
+            opts = 0
+        elif a.halo == "auto":
+            ok, why = verify_peer(M, s, make, rank)
+            if ok:
+                halo_note = why
+            else:
+                halo_note = f"peer halo rejected ({why}): rccl"
+                s.close()
+                opts = 0
+                s = make(M.SMOOTHER, 0, "sweep-rccl")
     def barrier():
         s.synchronize()
         if world > 1:
@@ -363,19 +413,9 @@ def main():
     kname = s.smooth_kernel_name(0)  # as rocprofv3 prints it (profiles/ are matched on it)
     s.close()
     # V-cycles/s (same volume, nu = 2) on a solver in the production layout (CycleType
-    # VCYCLE: level-0 records without b, dense rhs), as GenerateData runs it
-    s = M.Solver(shape, (1.0, 1.0, 1.0), time_step=0.1, smoother=sm, precision=M.FP32,
-                 cycle=M.VCYCLE,
-                 nranks=world, rank=rank, device=local if world > 1 else -1, global_shape=gshape,
-                 gs_kernel=a.gs_kernel, options=opts)
-    if world > 1:
-        phase(rank, "V-cycle solver: joining the communicator")
-        MD.bootstrap_node(s, rank, world, tag="vcycle")
-    phase(rank, "V-cycle solver: setup")
-    s.synth_tensor(kind=0, seed=4)
-    s.setup()
-    s.synth_level(0, M.capi.B, 3)
-    s.synth_level(0, M.capi.X, 3)
+    # VCYCLE: level-0 records without b, dense rhs), as GenerateData runs it; the halo form
+    # the sweep measurement settled on
+    s = make(M.VCYCLE, opts, "vcycle")
     s.vcycle()
     barrier()
     t1 = time.perf_counter()
@@ -430,7 +470,8 @@ def main():
                    "levels": nlev, "time_step": 0.1, "parallelism": f"z-slab x{world}",
                    "halo": (None if world == 1 else
                             ("peer: edge planes stored by the sweep into the neighbours' mailboxes"
-                             if "peer halo" in kname else "rccl: grouped send/recv after each sweep")),
+                             if "peer halo" in kname else "rccl: grouped send/recv after each sweep")
+                            + (f"; {halo_note}" if halo_note else "")),
                    "slab_shape": list(info["shape"])},
         "vcycles_per_s": round(a.vcycles / vwall, 3),
         "vcycle_config": "CycleType VCYCLE (dense rhs layout), nu = 2, 4-colour GS, "

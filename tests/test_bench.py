@@ -84,3 +84,56 @@ def test_gpus_must_match_world_size():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
                          capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+class _FakeSolver:
+    """Stands in for a rank's solver in verify_peer: `result` is what its slab holds after the
+    sweeps (None: the sweeps raise), `others_same` what the other ranks report."""
+    def __init__(self, result, others_same=True):
+        self.result, self.others_same, self.synth, self.closed = result, others_same, [], False
+
+    def smooth(self, level, sweeps):
+        if self.result is None:
+            raise RuntimeError("mailbox wait timed out")
+
+    def download(self, level, which):
+        return self.result.copy()
+
+    def allreduce(self, values, op="sum"):
+        assert op == "max"  # Solver.allreduce: "sum" or "max"
+        return [max(values[0], 0.0 if self.others_same else 1.0)]
+
+    def synth_level(self, level, which, seed):
+        self.synth.append((level, which, seed))
+
+    def synchronize(self):
+        pass
+
+    def close(self):
+        self.closed = True
+
+
+@pytest.mark.parametrize("case", ["equal", "differs", "raises", "other_rank"])
+def test_halo_auto_uses_peer_only_when_bitwise_equal(case):
+    """--halo auto (the default for N > 1): the peer halo is kept only when every rank's slab
+    after the check sweeps is bit-identical to the RCCL exchange's; a device error in the peer
+    sweeps is a rejection too, and the RCCL check solver is always closed."""
+    import types
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    x = np.arange(24, dtype=np.float32).reshape(2, 3, 4)
+    y = x.copy()
+    if case == "differs":
+        y[1, 2, 3] = np.nextafter(y[1, 2, 3], np.float32(1e9))
+    peer = _FakeSolver(None if case == "raises" else y)
+    ref = _FakeSolver(x, others_same=case != "other_rank")
+    M = types.SimpleNamespace(SMOOTHER=2, capi=types.SimpleNamespace(X=0))
+    ok, note = bench.verify_peer(M, peer, lambda cycle, opts, tag: ref, rank=1)
+    assert ref.closed and not peer.closed
+    assert ok == (case == "equal")
+    if ok:
+        assert peer.synth == [(0, 0, 3)] and "bitwise equal" in note
+    else:
+        assert peer.synth == []
+        assert {"differs": "this rank", "raises": "timed out", "other_rank": "another rank"}[case] in note
