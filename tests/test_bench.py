@@ -137,3 +137,36 @@ def test_halo_auto_uses_peer_only_when_bitwise_equal(case):
     else:
         assert peer.synth == []
         assert {"differs": "this rank", "raises": "timed out", "other_rank": "another rank"}[case] in note
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("halo", ["auto", "rccl"])
+def test_bench_two_ranks_on_one_gpu(halo):
+    """The driver's N > 1 launch (torch.distributed.run, one process per rank), rehearsed with
+    both ranks on device 0 (MAD_BENCH_SHARED_GPU: RCCL over its socket transport): the line is
+    printed once, by rank 0, and the default halo form is the peer halo only after its in-run
+    bitwise check against the RCCL exchange passed (bench.verify_peer)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, MAD_BENCH_SHARED_GPU="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--size", "256", "--steps", "4", "--warmup", "1", "--vcycles", "2",
+           "--no-cpu-baseline", "--no-precision-cycles", "--halo", halo]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["vcycles_per_s"] > 0
+    assert d["config"]["slab_shape"] == [128, 256, 256] and d["config"]["parallelism"] == "z-slab x2"
+    h = d["config"]["halo"]
+    if halo == "auto":
+        assert h.startswith("peer:") and "verified in this run" in h, h
+        assert "peer halo" in d["roofline"]["kernel"]
+    else:
+        assert h.startswith("rccl:") and "peer halo" not in d["roofline"]["kernel"], h
