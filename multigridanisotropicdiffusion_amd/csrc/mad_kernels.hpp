@@ -1712,30 +1712,41 @@ __global__ void __launch_bounds__(NT) resid_restrict3_k(
 // 8-slot LDS ring (only the ones not already there), and the fine values of the NEXT
 // group are loaded while this group is computed, so each thread keeps G loads in
 // flight (one plane at a time left the level-0 launch latency-bound at ~2.5 TB/s).
-template <typename T, int ADD, int TX, int TY, int G = 8>
+//
+// VX > 1: each thread owns VX consecutive fine points of its row (fine tile TX*VX x TY) and
+// moves them with one VX-wide load / store (the caller checks that rows, planes and the base
+// are VX-aligned and nx % VX == 0); per point the same taps and the same fma chain as VX = 1.
+template <typename T, int V>
+struct alignas(sizeof(T) * V) VecT {
+  T v[V];
+};
+template <typename T, int ADD, int TX, int TY, int G = 8, int VX = 1>
 __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coarse, Geo gc,
                                                      T* __restrict__ fine, Geo gf, int cx, int cy,
                                                      int cz, int ncz, int kc, int ntx, int kbase,
                                                      int kend) {
 #pragma clang fp contract(off)  // explicit fma: every transfer kernel rounds alike
   constexpr int NT = TX * TY;
-  constexpr int CXW = TX / 2 + 2, CYW = TY / 2 + 2, CP = CXW * CYW;
+  constexpr int FX = TX * VX;  // fine points per tile row
+  constexpr int CXW = FX / 2 + 2, CYW = TY / 2 + 2, CP = CXW * CYW;
   constexpr int NS = 8;           // ring slots
   constexpr int SPAN = G / 2 + 2;  // most coarse planes one group of G fine planes taps
   static_assert(SPAN <= NS && CP <= NT, "interp3_k ring geometry");
+  using V = VecT<T, VX>;
   __shared__ T ring[NS * CP];
   const int tiles = ntx * ((gf.ny + TY - 1) / TY);
   const int chunk = blockIdx.x / tiles;
   const int t = blockIdx.x - chunk * tiles;
   const int tyi = t / ntx, txi = t - (t / ntx) * ntx;
-  const int i0 = txi * TX, j0 = tyi * TY;
+  const int i0 = txi * FX, j0 = tyi * TY;
   const int tid = threadIdx.x;
-  const int i = i0 + tid % TX, j = j0 + tid / TX;
+  const int i = i0 + (tid % TX) * VX, j = j0 + tid / TX;
   const bool ok = i < gf.nx && j < gf.ny;
   const int cx0 = i0 / 2 - 1, cy0 = j0 / 2 - 1;  // coarse tile origin
-  int ix[2], iy[2];
-  T wx[2], wy[2];
-  itaps2<T>(min(i, gf.nx - 1), gc.nx, cx, ix, wx);
+  int ix[VX][2], iy[2];
+  T wx[VX][2], wy[2];
+#pragma unroll
+  for (int v = 0; v < VX; ++v) itaps2<T>(min(i + v, gf.nx - 1), gc.nx, cx, ix[v], wx[v]);
   itaps2<T>(min(j, gf.ny - 1), gc.ny, cy, iy, wy);
   const int ci = tid < CP ? tid : CP - 1;  // one ring element per thread (CP <= NT)
   const int c_off = min(max(cy0 + ci / CXW, 0), gc.ny - 1) * (int)gc.sy +
@@ -1745,11 +1756,17 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
   const int k0 = kbase + chunk * kc, k1 = min(k0 + kc, kend);
   const int64_t pxy = (int64_t)j * gf.sy + i;
   int last = INT_MIN;  // largest coarse plane (global) in the ring
-  T xc[G], xn[G];
-  auto load_fine = [&](int kk, T* dst) {
+  V xc[G], xn[G];
+  auto load_fine = [&](int kk, V* dst) {
 #pragma unroll
-    for (int q = 0; q < G; ++q)
-      dst[q] = (ADD && ok && kk + q < k1) ? fine[pxy + gf.sz * (int64_t)(kk + q)] : T(0);
+    for (int q = 0; q < G; ++q) {
+      if (ADD && ok && kk + q < k1) {
+        dst[q] = *reinterpret_cast<const V*>(fine + pxy + gf.sz * (int64_t)(kk + q));
+      } else {
+#pragma unroll
+        for (int v = 0; v < VX; ++v) dst[q].v[v] = T(0);
+      }
+    }
   };
   load_fine(k0, xc);
   for (int k = k0; k < k1; k += G) {
@@ -1776,23 +1793,24 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
       const int kk = k + q;
       if (kk > kl) break;
       itaps2<T>(kk + gf.zoff, ncz, cz, iz, wz);
-      T v = T(0);
+      V out;
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const T* pl = ring + (iz[c] & (NS - 1)) * CP - cx0;
-        T vz = T(0);
+      for (int x = 0; x < VX; ++x) {
+        T v = T(0);
 #pragma unroll
-        for (int bq = 0; bq < 2; ++bq) {
-          const T* row = pl + (iy[bq] - cy0) * CXW;
-          vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
+        for (int c = 0; c < 2; ++c) {
+          const T* pl = ring + (iz[c] & (NS - 1)) * CP - cx0;
+          T vz = T(0);
+#pragma unroll
+          for (int bq = 0; bq < 2; ++bq) {
+            const T* row = pl + (iy[bq] - cy0) * CXW;
+            vz = fma(wy[bq], fma(wx[x][1], row[ix[x][1]], wx[x][0] * row[ix[x][0]]), vz);
+          }
+          v = fma(wz[c], vz, v);
         }
-        v = fma(wz[c], vz, v);
+        out.v[x] = ADD ? xc[q].v[x] + v : v;
       }
-      if (ok) {
-        const int64_t p = pxy + gf.sz * (int64_t)kk;
-        if (ADD) fine[p] = xc[q] + v;
-        else fine[p] = v;
-      }
+      if (ok) *reinterpret_cast<V*>(fine + pxy + gf.sz * (int64_t)kk) = out;
     }
     __syncthreads();  // ring slots are reused by the next group
 #pragma unroll

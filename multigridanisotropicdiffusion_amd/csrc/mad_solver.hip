@@ -2508,24 +2508,38 @@ class Solver final : public SolverBase {
 
   // x[l] (+)= P x[l+1], 3D, z-marching (interp3_k): 64x16 fine columns, ~1024 blocks.
   // The coarse level may be a slab (ghost planes exchanged) or replicated (zoff 0).
+  // fine points per thread in x where rows, planes and the array are aligned to them
+#ifndef MAD_INTERP_VX
+#define MAD_INTERP_VX 2
+#endif
   void launch_interp3(int l, bool add, bool ghosts = false) {
+    LevelData<T>& F = lv_[l];
+    const int vx = (MAD_INTERP_VX > 1 && F.g.nx % 2 == 0 && F.g.sy % 2 == 0 && F.g.sz % 2 == 0 &&
+                    ((uintptr_t)F.x % (2 * sizeof(T))) == 0) ? 2 : 1;
+    if (vx == 2)
+      launch_interp3_v<2>(l, add, ghosts);
+    else
+      launch_interp3_v<1>(l, add, ghosts);
+  }
+  template <int VX>
+  void launch_interp3_v(int l, bool add, bool ghosts) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
     constexpr int TX = 64, TY = 16;
     const int kbase = (ghosts && F.g.zlo_ghost) ? -GHOST : 0;
     const int kend = (ghosts && F.g.zhi_ghost) ? F.g.nz + GHOST : F.g.nz;
     const int nk = kend - kbase;
-    const int ntx = (F.g.nx + TX - 1) / TX, nty = (F.g.ny + TY - 1) / TY;
+    const int ntx = (F.g.nx + TX * VX - 1) / (TX * VX), nty = (F.g.ny + TY - 1) / TY;
     int chunks = std::max(1, std::min((xfer_blocks() + ntx * nty - 1) / (ntx * nty), nk / 4));
     const int kc = (nk + chunks - 1) / chunks;
     chunks = (nk + kc - 1) / kc;
     const unsigned nb = (unsigned)(ntx * nty * chunks);
     const int ncz = (int)c_->geom[l + 1].n[2];
     if (add)
-      hipLaunchKernelGGL((interp3_k<T, 1, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
+      hipLaunchKernelGGL((interp3_k<T, 1, TX, TY, 8, VX>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
                          C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx, kbase, kend);
     else
-      hipLaunchKernelGGL((interp3_k<T, 0, TX, TY>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
+      hipLaunchKernelGGL((interp3_k<T, 0, TX, TY, 8, VX>), dim3(nb), dim3(TX * TY), 0, c_->stream, C.x,
                          C.g, F.x, F.g, C.cent[0], C.cent[1], C.cent[2], ncz, kc, ntx, kbase, kend);
   }
 
