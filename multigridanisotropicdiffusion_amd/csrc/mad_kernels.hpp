@@ -908,6 +908,9 @@ __global__ void __launch_bounds__(256) peer_pong_k(const T* mlo, const T* mhi, c
 // entry point that returns results: mad_run, the norms, downloads, mad_synchronize).
 // The mailboxes are uncached, so the copy reads what the neighbour stored; the ghost planes are
 // then ordinary stream-ordered data for the kernels that follow.
+#ifndef UNPACK_LOADS
+#define UNPACK_LOADS 8
+#endif
 __global__ void __launch_bounds__(256) peer_unpack_k(char* __restrict__ dlo, const char* __restrict__ slo,
                                                      char* __restrict__ dhi, const char* __restrict__ shi,
                                                      uint64_t bytes, uint32_t* __restrict__ ctl, int ci,
@@ -935,7 +938,21 @@ __global__ void __launch_bounds__(256) peer_unpack_k(char* __restrict__ dlo, con
       const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
       const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
       if ((((uintptr_t)d | (uintptr_t)src | bytes) & 15) == 0) {
-        for (uint64_t i = t0; i < bytes / 16; i += stride) ((uint4*)d)[i] = ((const uint4*)src)[i];
+        // UNPACK_LOADS 16-B loads in flight per thread before their stores: every read of the
+        // uncached mailbox goes to memory, and one load per iteration left the copy latency-bound
+        // (a 512^2 x 4-plane side per 64 blocks: 13.5 us per launch with one, 8.2-8.7 with eight, 9.3
+        // with sixteen; profiles/r05_unpack_ab.log)
+        constexpr int NL = UNPACK_LOADS;
+        const uint64_t n16 = bytes / 16;
+        uint64_t i = t0;
+        for (; i + (NL - 1) * stride < n16; i += NL * stride) {
+          uint4 v[NL];
+#pragma unroll
+          for (int q = 0; q < NL; ++q) v[q] = ((const uint4*)src)[i + q * stride];
+#pragma unroll
+          for (int q = 0; q < NL; ++q) ((uint4*)d)[i + q * stride] = v[q];
+        }
+        for (; i < n16; i += stride) ((uint4*)d)[i] = ((const uint4*)src)[i];
       } else {
         for (uint64_t i = t0; i < bytes / 4; i += stride) ((uint32_t*)d)[i] = ((const uint32_t*)src)[i];
       }
