@@ -2491,9 +2491,22 @@ class Solver final : public SolverBase {
     Geo gf{};
     gf.nx = (int)Gf.n[0]; gf.ny = (int)Gf.n[1]; gf.nz = (int)Gf.n[2];
     gf.sy = Gf.n[0]; gf.sz = Gf.n[0] * Gf.n[1]; gf.N = Gf.N;
-    dim3 gr = grid_for(C.g.nx, C.g.ny, C.g.nz, BLK);
-    hipLaunchKernelGGL((restrict_k<T, T, 3>), gr, BLK, 0, c_->stream, fine_full, gf, coarse, C.g,
-                       C.cent[0], C.cent[1], C.cent[2], 0);
+    if (c_->dim == 3) {
+      // z-marching (restrict3_k, the same taps and fma order as restrict_k): 64^3 from the gathered
+      // 128^3 of an 8-rank cycle in 8.0 instead of 12-17 us per cycle with one thread per coarse point
+      constexpr int CX = 32, CY = 8;
+      const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
+      int chunks = std::max(1, std::min((xfer_blocks() + ntx * nty - 1) / (ntx * nty), std::max(1, C.g.nz / 4)));
+      const int kc = (C.g.nz + chunks - 1) / chunks;
+      chunks = (C.g.nz + kc - 1) / kc;
+      hipLaunchKernelGGL((restrict3_k<T, T, CX, CY>), dim3((unsigned)(ntx * nty * chunks)), dim3(CX * CY), 0,
+                         c_->stream, fine_full, gf, coarse, C.g, C.cent[0], C.cent[1], C.cent[2], 0,
+                         (int)c_->geom[l + 1].n[2], kc, ntx);
+    } else {
+      dim3 gr = grid_for(C.g.nx, C.g.ny, C.g.nz, BLK);
+      hipLaunchKernelGGL((restrict_k<T, T, 3>), gr, BLK, 0, c_->stream, fine_full, gf, coarse, C.g,
+                         C.cent[0], C.cent[1], C.cent[2], 0);
+    }
     HIP_CHECK(hipGetLastError());
   }
 
