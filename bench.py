@@ -275,35 +275,41 @@ def load_traffic(tag, kernel_sig):
 T0 = time.perf_counter()
 
 
-def verify_peer(M, s, make, rank, sweeps=4):
-    """--halo auto: the peer-halo solver `s` and a second solver exchanging through RCCL sweep
-    the same synthetic system `sweeps` times (both mailbox buffers twice) and every rank compares
-    its slab bit for bit; the peer halo is used only if all ranks agree.  Collective: every rank
-    reaches the same allreduce whatever its own outcome.  Leaves `s` at the initial x again.
-    Returns (ok, note)."""
+def verify_peer(M, s, make, rank, steps=4, vcycles=False):
+    """--halo auto: the peer-halo solver `s` and a second solver exchanging through RCCL run the
+    same synthetic system -- `steps` level-0 sweeps (both mailbox buffers twice) or, with
+    `vcycles`, `steps` V-cycles (eager, captured, replayed: every distributed level's pushes and
+    unpacks) -- and every rank compares its slab bit for bit; the peer halo is used only if all
+    ranks agree.  Collective: every rank reaches the same allreduce whatever its own outcome.
+    Leaves `s` at the initial x again.  Returns (ok, note)."""
     import numpy as np
-    phase(rank, f"halo auto: {sweeps} peer sweeps vs {sweeps} rccl sweeps, bitwise")
+    what = "V-cycles" if vcycles else "sweeps"
+    phase(rank, f"halo auto: {steps} peer {what} vs {steps} rccl {what}, bitwise")
+
+    def run(sv):
+        for _ in range(steps if vcycles else 1):
+            sv.vcycle() if vcycles else sv.smooth(0, steps)
+        return sv.download(0, M.capi.X)
+
     err = None
     try:
-        s.smooth(0, sweeps)
-        xp = s.download(0, M.capi.X)
+        xp = run(s)
     except Exception as e:  # a timed-out mailbox wait (peer_check) or any device error
         err, xp = f"{type(e).__name__}: {e}"[:200], None
-    ref = make(M.SMOOTHER, 0, "halo-check")
-    ref.smooth(0, sweeps)
-    xr = ref.download(0, M.capi.X)
+    ref = make(M.VCYCLE if vcycles else M.SMOOTHER, 0, "vcycle-check" if vcycles else "halo-check")
+    xr = run(ref)
     same = xp is not None and xp.shape == xr.shape and np.array_equal(xp.view(np.uint32), xr.view(np.uint32))
     agree = float(ref.allreduce([0.0 if same else 1.0], "max")[0]) == 0.0
     ref.close()
     if agree:
         s.synth_level(0, M.capi.X, 3)
         s.synchronize()
-        return True, (f"verified in this run: {sweeps} sweeps bitwise equal to the rccl exchange on "
+        return True, (f"verified in this run: {steps} {what} bitwise equal to the rccl exchange on "
                       "every rank")
     if err:
         return False, f"rank {rank}: {err}"
     return False, ("this rank's slab differed from the rccl exchange" if not same
-                   else "another rank's slab differed from the rccl exchange, or its peer sweeps failed")
+                   else "another rank's slab differed from the rccl exchange, or its peer run failed")
 
 
 def phase(rank, what):
@@ -374,7 +380,7 @@ def main():
             halo_note = "peer halo requested, not engaged at setup (window mapping or self-test): rccl"
             opts = 0
         elif a.halo == "auto":
-            ok, why = verify_peer(M, s, make, rank)
+            ok, why = verify_peer(M, s, make, rank, steps=4)
             if ok:
                 halo_note = why
             else:
@@ -416,6 +422,15 @@ def main():
     # VCYCLE: level-0 records without b, dense rhs), as GenerateData runs it; the halo form
     # the sweep measurement settled on
     s = make(M.VCYCLE, opts, "vcycle")
+    vnote = None
+    if opts and a.halo == "auto":
+        # the V-cycle's distributed levels push too (per-colour levels after their last colour
+        # pass): checked against the RCCL exchange like the sweeps
+        ok, why = verify_peer(M, s, make, rank, steps=3, vcycles=True)
+        vnote = why if ok else f"V-cycle peer halo rejected ({why}): rccl"
+        if not ok:
+            s.close()
+            s = make(M.VCYCLE, 0, "vcycle-rccl")
     s.vcycle()
     barrier()
     t1 = time.perf_counter()
@@ -475,7 +490,7 @@ def main():
                    "slab_shape": list(info["shape"])},
         "vcycles_per_s": round(a.vcycles / vwall, 3),
         "vcycle_config": "CycleType VCYCLE (dense rhs layout), nu = 2, 4-colour GS, "
-                         f"{nlev} levels, graph-replayed per rank",
+                         f"{nlev} levels, graph-replayed per rank" + (f"; {vnote}" if vnote else ""),
         "device_ms_per_vcycle": round(vc_ms / a.vcycles, 3),
         "ms_per_vcycle": round(vwall / a.vcycles * 1e3, 3),
         "device_ms_per_step": round(dev_ms / a.steps, 4),

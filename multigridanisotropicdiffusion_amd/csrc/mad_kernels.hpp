@@ -911,6 +911,53 @@ __global__ void __launch_bounds__(256) peer_pong_k(const T* mlo, const T* mhi, c
 #ifndef UNPACK_LOADS
 #define UNPACK_LOADS 8
 #endif
+// grid-strided byte copy with UNPACK_LOADS loads in flight per thread before their stores (16-B
+// words where both ends and the length allow, else 4-B): a copy from (or into) the uncached
+// mailboxes is latency-bound with one load per iteration -- a 512^2 x 4-plane side per 64 blocks
+// took 13.5 us per unpack with one, 8.2-8.7 with eight, 9.3 with sixteen (profiles/r05_unpack_ab.log)
+template <typename W>
+__device__ __forceinline__ void copy_words(W* __restrict__ d, const W* __restrict__ s, uint64_t n,
+                                           uint64_t t0, uint64_t stride) {
+  constexpr int NL = UNPACK_LOADS;
+  uint64_t i = t0;
+  for (; i + (NL - 1) * stride < n; i += NL * stride) {
+    W v[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) v[q] = s[i + q * stride];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) d[i + q * stride] = v[q];
+  }
+  for (; i < n; i += stride) d[i] = s[i];
+}
+__device__ __forceinline__ void copy_inflight(char* d, const char* s, uint64_t bytes, uint64_t t0,
+                                              uint64_t stride) {
+  if ((((uintptr_t)d | (uintptr_t)s | bytes) & 15) == 0)
+    copy_words((uint4*)d, (const uint4*)s, bytes / 16, t0, stride);
+  else
+    copy_words((uint32_t*)d, (const uint32_t*)s, bytes / 4, t0, stride);
+}
+
+// Per-colour GS levels (rank slabs, MAD_OPT_PEER_HALO): after a sweep's last colour pass, the
+// GHOST edge planes of x into the neighbours' mailboxes of this batch's buffer (blockIdx.y = side:
+// 0 the bottom planes for rank - 1, 1 the top planes for rank + 1; po.dst[1] points at its
+// mailbox's last plane, where the fused sweep's reflected top chunk starts, so the push steps back
+// to the mailbox's first), then -- stores complete (vmcnt 0), barrier -- every workgroup counts
+// itself in the neighbour's counter with a relaxed system-scope increment: the fused sweep's and
+// peer_ping_k's completion pattern, resolved by the same peer_unpack_k (tiles = push blocks)
+template <typename T>
+__global__ void __launch_bounds__(256) peer_push_k(const T* __restrict__ x, int64_t top_off, PeerOut<T> po,
+                                                   int64_t n, int64_t top_dst_off) {
+  const int side = blockIdx.y;
+  T* dt = po.dst[side];
+  if (!dt) return;
+  char* d = (char*)(dt - (side ? top_dst_off : 0));
+  const char* s = (const char*)(x + (side ? top_off : 0));
+  copy_inflight(d, s, (uint64_t)n * sizeof(T), (uint64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                (uint64_t)gridDim.x * blockDim.x);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(po.sig[side], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ void __launch_bounds__(256) peer_unpack_k(char* __restrict__ dlo, const char* __restrict__ slo,
                                                      char* __restrict__ dhi, const char* __restrict__ shi,
                                                      uint64_t bytes, uint32_t* __restrict__ ctl, int ci,
@@ -937,25 +984,7 @@ __global__ void __launch_bounds__(256) peer_unpack_k(char* __restrict__ dlo, con
     if (!failed) {
       const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
       const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-      if ((((uintptr_t)d | (uintptr_t)src | bytes) & 15) == 0) {
-        // UNPACK_LOADS 16-B loads in flight per thread before their stores: every read of the
-        // uncached mailbox goes to memory, and one load per iteration left the copy latency-bound
-        // (a 512^2 x 4-plane side per 64 blocks: 13.5 us per launch with one, 8.2-8.7 with eight, 9.3
-        // with sixteen; profiles/r05_unpack_ab.log)
-        constexpr int NL = UNPACK_LOADS;
-        const uint64_t n16 = bytes / 16;
-        uint64_t i = t0;
-        for (; i + (NL - 1) * stride < n16; i += NL * stride) {
-          uint4 v[NL];
-#pragma unroll
-          for (int q = 0; q < NL; ++q) v[q] = ((const uint4*)src)[i + q * stride];
-#pragma unroll
-          for (int q = 0; q < NL; ++q) ((uint4*)d)[i + q * stride] = v[q];
-        }
-        for (; i < n16; i += stride) ((uint4*)d)[i] = ((const uint4*)src)[i];
-      } else {
-        for (uint64_t i = t0; i < bytes / 4; i += stride) ((uint32_t*)d)[i] = ((const uint32_t*)src)[i];
-      }
+      copy_inflight(d, src, bytes, t0, stride);
     }
   }
   if (threadIdx.x == 0) {

@@ -311,7 +311,12 @@ struct LevelData {
   bool win_ipc = false;
   bool peer = false;
   bool x_peer_pending = false;  // x's ghost planes arrive by peer stores: resolve before use
-  uint32_t peer_tiles = 0;
+  uint32_t peer_tiles = 0;      // counts per side and batch (fused: edge tiles; per-colour: push blocks)
+  // per-colour levels (round 5): after a sweep's last colour pass peer_push_k copies the edge planes
+  // into the neighbours' mailboxes; the batches alternate between the two buffers by peer_seq
+  bool peer_pc = false;
+  int peer_seq = 0;
+  int peer_buf = 0;  // buffer of the batch in flight (x_peer_pending)
 };
 // z-depth of a rank slab's boundary chunks (>= GHOST; 4 measured 0.231 vs 0.228 ms per 8-rank
 // sweep, profiles/r02_slab_tiles.log)
@@ -460,7 +465,9 @@ class Solver final : public SolverBase {
   bool peer_eligible(int l) {
     LevelData<T>& L = lv_[l];
     if (!(c_->d.options & MAD_OPT_PEER_HALO) || !c_->comm.active() || !c_->geom[l].distributed) return false;
-    if (!use_fused(l) || c_->dim != 3) return false;
+    if (c_->dim != 3) return false;
+    if (!use_fused(l))  // per-colour GS level: pushed after its last colour pass (peer_push)
+      return c_->d.smoother == MAD_GAUSS_SEIDEL && colour_ca(l) && L.g.nz >= GHOST;
     int tiles = 0, nchunks = 0;
     fused_shape(L, &tiles, &nchunks);
     const ZRange zr = whole_range(L.g.nz, tiles, fused_cfg());
@@ -499,9 +506,14 @@ class Solver final : public SolverBase {
         peer_fallbacks_ += 1;
         continue;
       }
-      int tiles = 0, nchunks = 0;
-      fused_shape(L, &tiles, &nchunks);
-      L.peer_tiles = (uint32_t)tiles;
+      if (use_fused((int)l)) {
+        int tiles = 0, nchunks = 0;
+        fused_shape(L, &tiles, &nchunks);
+        L.peer_tiles = (uint32_t)tiles;
+      } else {
+        L.peer_pc = true;
+        L.peer_tiles = push_blocks(L);
+      }
       L.peer = true;
     }
   }
@@ -565,7 +577,7 @@ class Solver final : public SolverBase {
     LevelData<T>& L = lv_[l];
     if (!L.x_peer_pending) return;
     L.x_peer_pending = false;
-    const int buf = buffer_index(L, L.x);
+    const int buf = L.peer_buf;
     if (c_->comm.mode() == Comm::LOCAL) c_->comm.local_barrier(c_->stream);
     const size_t bytes = (size_t)L.ghost * sizeof(T);
     char* dlo = L.g.zlo_ghost ? (char*)(L.x - L.ghost) : nullptr;
@@ -580,6 +592,26 @@ class Solver final : public SolverBase {
   }
   void peer_resolve_all() {
     for (size_t l = 0; l < lv_.size(); ++l) peer_resolve((int)l);
+  }
+  // per-colour levels: workgroups per side of peer_push_k (each counts itself in when its stores
+  // are complete), as many as the unpack uses
+  static uint32_t push_blocks(const LevelData<T>& L) {
+    const size_t bytes = (size_t)L.ghost * sizeof(T);
+    return (uint32_t)std::min<size_t>(64, std::max<size_t>(1, (bytes / 16 + 255) / 256));
+  }
+  // after the last colour pass of a per-colour sweep: the GHOST edge planes into the neighbours'
+  // mailboxes of the next buffer, no exchange; the next consumer of x's ghost planes resolves it
+  void peer_push(int l) {
+    LevelData<T>& L = lv_[l];
+    const int buf = L.peer_seq & 1;
+    ++L.peer_seq;
+    const int64_t top_off = (int64_t)(L.g.nz - GHOST) * L.g.sz;
+    hipLaunchKernelGGL((peer_push_k<T>), dim3(push_blocks(L), 2), dim3(256), 0, c_->stream, L.x, top_off,
+                       peer_out(L, buf), (int64_t)L.ghost, (int64_t)(GHOST - 1) * L.g.sz);
+    HIP_CHECK(hipGetLastError());
+    L.peer_buf = buf;
+    L.x_halo_ok = true;
+    L.x_peer_pending = true;
   }
   void check_device_errors() override { peer_check(); }
   // a peer wait that timed out (a neighbour never delivered) is an error, not silent stale halos
@@ -952,6 +984,7 @@ class Solver final : public SolverBase {
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
     if (L.peer) {
       // the sweep delivers its edge planes to the neighbours itself; no exchange follows
+      L.peer_buf = buffer_index(L, L.t);
       launch_fused_part(L, 4);
       if (e1) HIP_CHECK(hipEventRecord(e1, c_->stream));
       std::swap(L.x, L.t);
@@ -1097,7 +1130,10 @@ class Solver final : public SolverBase {
                                  L.cf, L.g, L.rat, col, nc, k0);
             });
           }
-          x_changed(l);
+          if (L.peer)
+            peer_push(l);
+          else
+            x_changed(l);
         } else {
           dim3 gr = grid_for((L.g.nx + 1) / 2, rows, L.g.nz, BLK);
           for (int col = 0; col < nc; ++col) {
@@ -1558,7 +1594,8 @@ class Solver final : public SolverBase {
       // so it is re-captured for the current pointers
       bool same = vgraph_ptrs_.size() == lv_.size() && vgraph_zu_ == zu;
       for (size_t l = 0; same && l < lv_.size(); ++l)
-        same = vgraph_ptrs_[l].first == lv_[l].x && vgraph_ptrs_[l].second == lv_[l].t;
+        same = vgraph_ptrs_[l].first == lv_[l].x && vgraph_ptrs_[l].second == lv_[l].t &&
+               vgraph_seq_[l] == (lv_[l].peer_seq & 1);  // per-colour peer levels: mailbox parity
       if (!same) {
         HIP_CHECK(hipStreamSynchronize(c_->stream));
         (void)hipGraphExecDestroy(vgraph_);
@@ -1572,10 +1609,11 @@ class Solver final : public SolverBase {
         T* a0;
         T* a3;
         bool bh;
+        int seq;
       };
       auto snap = [&] {
         std::vector<Snap> v;
-        for (auto& L : lv_) v.push_back({L.x, L.t, L.alloc[0], L.alloc[3], L.b_halo_ok});
+        for (auto& L : lv_) v.push_back({L.x, L.t, L.alloc[0], L.alloc[3], L.b_halo_ok, L.peer_seq});
         return v;
       };
       auto restore = [&](const std::vector<Snap>& v) {
@@ -1585,6 +1623,7 @@ class Solver final : public SolverBase {
           lv_[l].alloc[0] = v[l].a0;
           lv_[l].alloc[3] = v[l].a3;
           lv_[l].b_halo_ok = v[l].bh;
+          lv_[l].peer_seq = v[l].seq;
         }
       };
       const std::vector<Snap> before = snap();
@@ -1612,8 +1651,11 @@ class Solver final : public SolverBase {
       }
       const std::vector<Snap> after = snap();
       bool same = captured;
+      // (a cycle pushes a per-colour peer level's batches an even number of times, 2 nu: a replay
+      // leaves the mailbox parity where the capture found it)
       for (size_t l = 0; same && l < before.size(); ++l)
-        same = before[l].x == after[l].x && before[l].t == after[l].t;
+        same = before[l].x == after[l].x && before[l].t == after[l].t &&
+               ((before[l].seq ^ after[l].seq) & 1) == 0;
       vgraph_exit_flags_ = halo_flags();  // the bookkeeping one cycle leaves
       restore(before);  // capture issued nothing: the state must not advance
       if (ranks) {
@@ -1639,7 +1681,11 @@ class Solver final : public SolverBase {
       vgraph_zu_ = zu;
       zero_x0_ = false;
       vgraph_ptrs_.clear();
-      for (auto& L : lv_) vgraph_ptrs_.emplace_back(L.x, L.t);
+      vgraph_seq_.clear();
+      for (auto& L : lv_) {
+        vgraph_ptrs_.emplace_back(L.x, L.t);
+        vgraph_seq_.push_back(L.peer_seq & 1);
+      }
     }
     HIP_CHECK(hipGraphLaunch(vgraph_, c_->stream));
     zero_x0_ = false;
@@ -2079,6 +2125,7 @@ class Solver final : public SolverBase {
   hipGraphExec_t vgraph_ = nullptr;  // captured V-cycle (vcycle_fast)
   bool vgraph_zu_ = false;            // its first level-0 sweep is the zero-iterate form
   std::vector<std::pair<T*, T*>> vgraph_ptrs_;  // per-level (x, t) the graph was captured with
+  std::vector<int> vgraph_seq_;                  // per-level peer mailbox parity it was captured with
   bool vgraph_failed_ = false;
   uint64_t peer_timeout_ticks_ = 0;
   int peer_fallbacks_ = 0;  // levels whose peer self-test failed (they exchange instead)
@@ -2114,6 +2161,7 @@ class Solver final : public SolverBase {
     if (vgraph_) (void)hipGraphExecDestroy(vgraph_);
     vgraph_ = nullptr;
     vgraph_ptrs_.clear();
+    vgraph_seq_.clear();
     vgraph_failed_ = false;
     vcycles_eager_ = 0;
     for (auto& L : lv_) {

@@ -96,6 +96,11 @@ class _FakeSolver:
         if self.result is None:
             raise RuntimeError("mailbox wait timed out")
 
+    def vcycle(self):
+        self.cycles = getattr(self, "cycles", 0) + 1
+        if self.result is None:
+            raise RuntimeError("mailbox wait timed out")
+
     def download(self, level, which):
         return self.result.copy()
 
@@ -113,8 +118,9 @@ class _FakeSolver:
         self.closed = True
 
 
+@pytest.mark.parametrize("vcycles", [False, True])
 @pytest.mark.parametrize("case", ["equal", "differs", "raises", "other_rank"])
-def test_halo_auto_uses_peer_only_when_bitwise_equal(case):
+def test_halo_auto_uses_peer_only_when_bitwise_equal(case, vcycles):
     """--halo auto (the default for N > 1): the peer halo is kept only when every rank's slab
     after the check sweeps is bit-identical to the RCCL exchange's; a device error in the peer
     sweeps is a rejection too, and the RCCL check solver is always closed."""
@@ -128,9 +134,18 @@ def test_halo_auto_uses_peer_only_when_bitwise_equal(case):
         y[1, 2, 3] = np.nextafter(y[1, 2, 3], np.float32(1e9))
     peer = _FakeSolver(None if case == "raises" else y)
     ref = _FakeSolver(x, others_same=case != "other_rank")
-    M = types.SimpleNamespace(SMOOTHER=2, capi=types.SimpleNamespace(X=0))
-    ok, note = bench.verify_peer(M, peer, lambda cycle, opts, tag: ref, rank=1)
+    M = types.SimpleNamespace(SMOOTHER=2, VCYCLE=0, capi=types.SimpleNamespace(X=0))
+    made = []
+
+    def make(cycle, opts, tag):
+        made.append((cycle, opts))
+        return ref
+
+    ok, note = bench.verify_peer(M, peer, make, rank=1, steps=3, vcycles=vcycles)
+    assert made == [(0 if vcycles else 2, 0)]  # the reference solver exchanges through RCCL
     assert ref.closed and not peer.closed
+    if vcycles:
+        assert ref.cycles == 3 and (case == "raises" or peer.cycles == 3)
     assert ok == (case == "equal")
     if ok:
         assert peer.synth == [(0, 0, 3)] and "bitwise equal" in note
@@ -168,5 +183,7 @@ def test_bench_two_ranks_on_one_gpu(halo):
     if halo == "auto":
         assert h.startswith("peer:") and "verified in this run" in h, h
         assert "peer halo" in d["roofline"]["kernel"]
+        # the V-cycle solver's peer levels (the per-colour ones included) checked the same way
+        assert "verified in this run: 3 V-cycles" in d["vcycle_config"], d["vcycle_config"]
     else:
         assert h.startswith("rccl:") and "peer halo" not in d["roofline"]["kernel"], h
