@@ -7,7 +7,9 @@ copies the mailbox out and resets the counters; the next sweep starts after that
 interleavings and 2 / 3 / 5 ranks: every copy sees exactly the neighbour's sweep-k planes (a mailbox
 is never overwritten before it was copied out), and no counter ever holds more than one batch (a
 reset never loses a signal).  The GPU tests check the kernels; this checks the ordering argument in
-DESIGN.md ("Peer halo")."""
+DESIGN.md ("Peer halo").  The per-colour levels' push (peer_push_k after the last colour pass, round
+5) is the same sequence -- store, count, the neighbour's unpack before the next push -- with the
+buffer chosen by a per-level push counter instead of the ping-pong pair's identity."""
 import random
 import threading
 
