@@ -317,6 +317,9 @@ struct LevelData {
   bool peer_pc = false;
   int peer_seq = 0;
   int peer_buf = 0;  // buffer of the batch in flight (x_peer_pending)
+  // b of a distributed coarse level: the descent pushes its edge planes (one buffer, mailboxes
+  // [4 + side], counters [8 + side]); the first sweep takes them in
+  bool b_peer_pending = false;
 };
 // z-depth of a rank slab's boundary chunks (>= GHOST; 4 measured 0.231 vs 0.228 ms per 8-rank
 // sweep, profiles/r02_slab_tiles.log)
@@ -455,12 +458,13 @@ class Solver final : public SolverBase {
   // neighbours' counters and copies the mailboxes in (peer_resolve, one small launch).  Collective
   // (share_window); every rank takes the same decision (same plane counts on distributed levels).
   static constexpr size_t PEER_CTL = 256;
-  size_t window_bytes(const LevelData<T>& L) const { return 4 * (size_t)L.ghost * sizeof(T) + PEER_CTL; }
+  // six mailboxes of GHOST planes: x [buffer * 2 + side] (buffers 0, 1), b [4 + side]; then the control block
+  size_t window_bytes(const LevelData<T>& L) const { return 6 * (size_t)L.ghost * sizeof(T) + PEER_CTL; }
   T* mailbox(char* w, const LevelData<T>& L, int buf, int side) const {
     return (T*)(w + (size_t)(buf * 2 + side) * (size_t)L.ghost * sizeof(T));
   }
   uint32_t* peer_ctl(char* w, const LevelData<T>& L) const {
-    return (uint32_t*)(w + 4 * (size_t)L.ghost * sizeof(T));
+    return (uint32_t*)(w + 6 * (size_t)L.ghost * sizeof(T));
   }
   bool peer_eligible(int l) {
     LevelData<T>& L = lv_[l];
@@ -554,18 +558,20 @@ class Solver final : public SolverBase {
   // own mailbox of its own side, as SOLO's exchange copies the own edge planes into the own ghost
   // planes -- the same bytes, and a rank at either end of the decomposition waits only on the side
   // it has
+  // (buf 2: the b mailboxes, counted in counters 8 + side)
   PeerOut<T> peer_out(const LevelData<T>& L, int buf) const {
     PeerOut<T> po{{nullptr, nullptr}, {nullptr, nullptr}};
     const bool self = c_->comm.stand_in();
+    const int cbase = buf == 2 ? 8 : buf * 2;
     if (L.g.zlo_ghost && L.win_lo) {
       const int side = self ? 0 : 1;
       po.dst[0] = mailbox(L.win_lo, L, buf, side);
-      po.sig[0] = peer_ctl(L.win_lo, L) + buf * 2 + side;
+      po.sig[0] = peer_ctl(L.win_lo, L) + cbase + side;
     }
     if (L.g.zhi_ghost && L.win_hi) {
       const int side = self ? 1 : 0;
       po.dst[1] = mailbox(L.win_hi, L, buf, side) + (int64_t)(GHOST - 1) * L.g.sz;
-      po.sig[1] = peer_ctl(L.win_hi, L) + buf * 2 + side;
+      po.sig[1] = peer_ctl(L.win_hi, L) + cbase + side;
     }
     return po;
   }
@@ -591,7 +597,53 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipGetLastError());
   }
   void peer_resolve_all() {
-    for (size_t l = 0; l < lv_.size(); ++l) peer_resolve((int)l);
+    for (size_t l = 0; l < lv_.size(); ++l) {
+      peer_resolve((int)l);
+      peer_resolve_b((int)l);
+    }
+  }
+  // b's ghost planes from the neighbours' descents (counters 8 + side, mailboxes [4 + side])
+  void peer_resolve_b(int l) {
+    LevelData<T>& L = lv_[l];
+    if (!L.b_peer_pending) return;
+    L.b_peer_pending = false;
+    if (c_->comm.mode() == Comm::LOCAL) c_->comm.local_barrier(c_->stream);
+    const size_t bytes = (size_t)L.ghost * sizeof(T);
+    char* dlo = L.g.zlo_ghost ? (char*)(L.b - L.ghost) : nullptr;
+    char* dhi = L.g.zhi_ghost ? (char*)(L.b + (int64_t)L.g.nz * L.g.sz) : nullptr;
+    const unsigned blocks = push_blocks(L);
+    hipLaunchKernelGGL(peer_unpack_k, dim3(blocks, 2), dim3(256), 0, c_->stream, dlo,
+                       (const char*)mailbox(L.win, L, 2, 0), dhi, (const char*)mailbox(L.win, L, 2, 1),
+                       (uint64_t)bytes, peer_ctl(L.win, L), 8, blocks, peer_timeout_ticks_);
+    HIP_CHECK(hipGetLastError());
+  }
+  // the descent wrote b of a distributed peer level: its edge planes into the neighbours' b mailboxes
+  // (one buffer: the neighbour has taken in the previous cycle's batch before this rank's next
+  // descent can run -- this rank's level-l work in between waits for the neighbour's first sweep
+  // there, which starts with that unpack)
+  void peer_push_b(int l) {
+    LevelData<T>& L = lv_[l];
+    const int64_t top_off = (int64_t)(L.g.nz - GHOST) * L.g.sz;
+    hipLaunchKernelGGL((peer_push_k<T>), dim3(push_blocks(L), 2), dim3(256), 0, c_->stream, L.b, top_off,
+                       peer_out(L, 2), (int64_t)L.ghost, (int64_t)(GHOST - 1) * L.g.sz);
+    HIP_CHECK(hipGetLastError());
+    L.b_halo_ok = true;
+    L.b_peer_pending = true;
+  }
+  // b's ghost planes current for a sweep / descent on a rank slab: the pushed batch, or an exchange
+  void b_halo(int l) {
+    LevelData<T>& L = lv_[l];
+    if (L.b_peer_pending) peer_resolve_b(l);
+    if (!L.b_halo_ok) {
+      halo(l, L.b, GHOST);
+      L.b_halo_ok = true;
+    }
+  }
+  // level l's b is about to change (a batch still in flight for it is taken in first)
+  void b_changed(int l) {
+    LevelData<T>& L = lv_[l];
+    if (L.b_peer_pending) peer_resolve_b(l);
+    L.b_halo_ok = L.brec_ok = false;
   }
   // per-colour levels: workgroups per side of peer_push_k (each counts itself in when its stores
   // are complete), as many as the unpack uses
@@ -635,7 +687,7 @@ class Solver final : public SolverBase {
 
   void upload(int l, int which, const double* h) override {
     LevelData<T>& L = lv_[l];
-    if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
+    if (which == MAD_B) b_changed(l);
     if (which == MAD_X) x_changed(l);
     double* tmp = scratch64(L.g.N);
     HIP_CHECK(hipMemcpyAsync(tmp, h, sizeof(double) * L.g.N, hipMemcpyHostToDevice, c_->stream));
@@ -658,7 +710,7 @@ class Solver final : public SolverBase {
 
   void fill(int l, int which, double v) override {
     LevelData<T>& L = lv_[l];
-    if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
+    if (which == MAD_B) b_changed(l);
     if (which == MAD_X) x_changed(l);
     hipLaunchKernelGGL((fill_k<T>), dim3(flat_blocks(L.g.N)), dim3(256), 0, c_->stream, arr(l, which),
                        L.g.N, (T)v);
@@ -667,7 +719,7 @@ class Solver final : public SolverBase {
 
   void synth_level(int l, int which, uint64_t seed) override {
     LevelData<T>& L = lv_[l];
-    if (which == MAD_B) L.b_halo_ok = L.brec_ok = false;
+    if (which == MAD_B) b_changed(l);
     if (which == MAD_X) x_changed(l);
     const LevelGeom& G = c_->geom[l];
     hipLaunchKernelGGL((synth_image_k<T>), grid_for(L.g.nx, L.g.ny, L.g.nz, BLK), BLK, 0, c_->stream,
@@ -977,9 +1029,8 @@ class Solver final : public SolverBase {
     halo(l, L.x, GHOST);
     if (L.brec) {
       sync_brec(l);
-    } else if (!L.b_halo_ok) {
-      halo(l, L.b, GHOST);
-      L.b_halo_ok = true;
+    } else {
+      b_halo(l);
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
     if (L.peer) {
@@ -1117,10 +1168,7 @@ class Solver final : public SolverBase {
           // outermost of them reads ghost plane nc), so every later colour finds its ghost
           // neighbours updated -- the fused sweep's scheme
           halo(l, L.x, nc);
-          if (!L.b_halo_ok) {
-            halo(l, L.b, GHOST);
-            L.b_halo_ok = true;
-          }
+          b_halo(l);
           for (int col = 0; col < nc; ++col) {
             const int ext = nc - 1 - col;
             const int k0 = L.g.zlo_ghost ? -ext : 0, k1 = L.g.nz + (L.g.zhi_ghost ? ext : 0);
@@ -1327,20 +1375,34 @@ class Solver final : public SolverBase {
     // taps past the slab residualise the fine ghost planes: x and b ghost planes made current
     // first -- the b exchange stands in for the residual's)
     const bool dist = c_->geom[l].distributed;
-    if (c_->dim != 3 || dist != c_->geom[l + 1].distributed || F.g.nx < 16 || F.g.ny < 16 || F.g.nz < 2)
+    // the agglomeration hand-over (distributed l, replicated l + 1) where the z coarsening is
+    // cell-centred and splits evenly: every rank restricts its own slab into its coarse planes
+    // (a slab view of the coarse level), then the ranks all-gather those -- 1/8 of the bytes of the
+    // fine residual the other path gathers, and one pass instead of residual + restriction
+    const LevelGeom& Gc = c_->geom[l + 1];
+    const bool handover = dist && !Gc.distributed && C.cent[2] == 1 && F.g.nz % 2 == 0 &&
+                          F.g.zoff % 2 == 0 && (int64_t)(F.g.nz / 2) * c_->comm.nranks() == (int64_t)Gc.n[2];
+    if (c_->dim != 3 || (dist != Gc.distributed && !handover) || F.g.nx < 16 || F.g.ny < 16 || F.g.nz < 2)
       return false;
     if (dist) {
       halo(l, F.x, GHOST);
-      if (!F.brec && !F.b_halo_ok) {
-        halo(l, F.b, GHOST);
-        F.b_halo_ok = true;
-      }
+      if (!F.brec) b_halo(l);
     }
     sync_brec(l);
-    C.b_halo_ok = C.brec_ok = false;
-    T* zx = zero_x ? C.x : nullptr;
+    b_changed(l + 1);
+    T* zx = (zero_x && !handover) ? C.x : nullptr;
     // the kernel zeroes a rank slab's coarse x ghost planes too (the neighbours' zeros)
-    if (zero_x) C.x_halo_ok = dist;
+    if (zero_x && !handover) C.x_halo_ok = dist;
+    // where the coarse planes go: the coarse level, or (hand-over) this rank's planes of it
+    T* cb = C.b;
+    Geo gcv = C.g;
+    if (handover) {
+      gcv.nz = F.g.nz / 2;
+      gcv.zoff = F.g.zoff / 2;
+      gcv.N = gcv.sz * gcv.nz;
+      gcv.zlo_ghost = gcv.zhi_ghost = 0;
+      cb = coarse_slab((int64_t)gcv.N);
+    }
     // 32 x 8 coarse tiles in 512-thread blocks, two per CU (one block's barriers overlap the
     // other's loads), ~1024 blocks: 1.133 vs 1.177 ms per 512^3 launch with 1024-thread blocks
     // (profiles/r01_rr_nt_prof.log, r01_rr_blocks_prof.log)
@@ -1348,25 +1410,25 @@ class Solver final : public SolverBase {
     const int ncz = (int)c_->geom[l + 1].n[2];  // global coarse nz (taps in global indices)
     auto run = [&](auto CXc, auto CYc, auto NTc) {
       constexpr int CX = decltype(CXc)::value, CY = decltype(CYc)::value, NT = decltype(NTc)::value;
-      const int ntx = (C.g.nx + CX - 1) / CX, nty = (C.g.ny + CY - 1) / CY;
+      const int ntx = (gcv.nx + CX - 1) / CX, nty = (gcv.ny + CY - 1) / CY;
       // small coarse levels (<= 65536 voxels): one coarse plane per workgroup (a few tiles per plane
       // cannot fill the chip, and each z-step of the march is a serial round trip): 8^3..32^3 descents
       // 17.7 / 19.3 / 21.3 -> 9.6 / 9.7 / 10.9 us; at 64^3 it costs (27.2 -> 36.4 us), so 4 planes stay
       // the minimum there (profiles/r04_rr_chunk_ab.md)
-      const int zdiv = C.g.N <= MAD_RR_SMALL_VOXELS ? 1 : 4;
-      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), C.g.nz / zdiv));
-      const int kc = (C.g.nz + chunks - 1) / chunks;
-      chunks = (C.g.nz + kc - 1) / kc;
+      const int zdiv = gcv.N <= MAD_RR_SMALL_VOXELS ? 1 : 4;
+      int chunks = std::max(1, std::min((target + ntx * nty - 1) / (ntx * nty), gcv.nz / zdiv));
+      const int kc = (gcv.nz + chunks - 1) / chunks;
+      chunks = (gcv.nz + kc - 1) / kc;
       const dim3 grid((unsigned)(ntx * nty * chunks)), block(NT);
       auto go = [&](auto K) {
         constexpr int KD = decltype(K)::value;
         if (F.brec)
           hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT, true>), grid, block, 0, c_->stream,
-                             F.x, F.b, F.cf, F.g, F.rat, C.b, zx, C.g, C.cent[0], C.cent[1], C.cent[2],
+                             F.x, F.b, F.cf, F.g, F.rat, cb, zx, gcv, C.cent[0], C.cent[1], C.cent[2],
                              kc, ntx, F.g.zoff, ncz);
         else
           hipLaunchKernelGGL((resid_restrict3_k<T, KD, CX, CY, NT>), grid, block, 0, c_->stream, F.x,
-                             F.b, F.cf, F.g, F.rat, C.b, zx, C.g, C.cent[0], C.cent[1], C.cent[2], kc,
+                             F.b, F.cf, F.g, F.rat, cb, zx, gcv, C.cent[0], C.cent[1], C.cent[2], kc,
                              ntx, F.g.zoff, ncz);
       };
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
@@ -1378,13 +1440,19 @@ class Solver final : public SolverBase {
     run(std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{},
         std::integral_constant<int, 512>{});
     HIP_CHECK(hipGetLastError());
+    if (handover) {
+      wait_all_pending();
+      c_->comm.allgather_slabs(cb, C.b, (int64_t)gcv.nx * gcv.ny, (int64_t)Gc.n[2], sizeof(T), c_->stream);
+      if (zero_x) fill(l + 1, MAD_X, 0.0);
+    }
+    if (dist && C.peer) peer_push_b(l + 1);  // the neighbours' b ghost planes, no exchange
     return true;
   }
 
   void restrict_arr(int l, T* fine, T* coarse) {
     LevelData<T>& F = lv_[l];
     LevelData<T>& C = lv_[l + 1];
-    C.b_halo_ok = C.brec_ok = false;
+    b_changed(l + 1);
     REQUIRE(!c_->geom[l].distributed || c_->geom[l + 1].distributed, MAD_ERR_UNSUPPORTED,
             "restriction onto a replicated level");
     halo(l, fine);
@@ -2143,6 +2211,8 @@ class Solver final : public SolverBase {
   T* gathered_ = nullptr;
   T* full_x_ = nullptr;
   int64_t gathered_cap_ = 0;
+  T* cslab_ = nullptr;  // coarse_slab
+  int64_t cslab_cap_ = 0;
 
   void release() {
     if (c_ && c_->comm_stream) (void)hipStreamSynchronize(c_->comm_stream);
@@ -2188,6 +2258,9 @@ class Solver final : public SolverBase {
     cblk_.release();
     if (scratch_) (void)hipFree(scratch_);
     if (gathered_) (void)hipFree(gathered_);
+    if (cslab_) (void)hipFree(cslab_);
+    cslab_ = nullptr;
+    cslab_cap_ = 0;
     if (full_x_) (void)hipFree(full_x_);
     part_ = scal_ = hscal_ = inv_ = nullptr;
     scratch_ = nullptr;
@@ -2524,6 +2597,16 @@ class Solver final : public SolverBase {
     }
   }
 
+  // this rank's planes of the first replicated level (the hand-over descent, resid_restrict)
+  T* coarse_slab(int64_t n) {
+    if (n > cslab_cap_) {
+      if (cslab_) HIP_CHECK(hipFree(cslab_));
+      HIP_CHECK(hipMalloc(&cslab_, sizeof(T) * n));
+      cslab_cap_ = n;
+    }
+    return cslab_;
+  }
+
   // all ranks assemble the full level-l array from their slabs
   void gather_level(int l, const T* a) {
     const LevelGeom& G = c_->geom[l];
@@ -2535,7 +2618,7 @@ class Solver final : public SolverBase {
   void restrict_full(int l, const T* fine_full, T* coarse) {
     const LevelGeom& Gf = c_->geom[l];
     LevelData<T>& C = lv_[l + 1];
-    C.b_halo_ok = C.brec_ok = false;
+    b_changed(l + 1);
     Geo gf{};
     gf.nx = (int)Gf.n[0]; gf.ny = (int)Gf.n[1]; gf.nz = (int)Gf.n[2];
     gf.sy = Gf.n[0]; gf.sz = Gf.n[0] * Gf.n[1]; gf.N = Gf.N;
