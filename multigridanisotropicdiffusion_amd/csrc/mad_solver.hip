@@ -951,6 +951,7 @@ class Solver final : public SolverBase {
       std::snprintf(buf, sizeof buf, "gs_lex_plane_k<%s, %d, %d>", tn, dim, kind);
     } else if (!use_fused(l)) {
       std::snprintf(buf, sizeof buf, "gs_color_k<%s, %d, %d>", tn, dim, kind);
+      if (lv_[l].peer) return std::string(buf) + " [rank slab: peer halo, edge planes pushed after the last colour pass]";
     } else {
       const int tx = 64, ty = (kind == KFULL && sizeof(T) == 4) ? 32 : 16;
       const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : 1024;

@@ -336,3 +336,48 @@ def test_solo_peer_halo_end_ranks(rank):
             s.vcycle()
         assert np.isfinite(s.download(0, M.capi.X)).all()
         s.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_per_colour_peer_halo_bitwise(nranks, precision):
+    """MAD_OPT_PEER_HALO with the default kernels (round 5): on these small levels every distributed
+    level sweeps colour by colour, so each sweep pushes its edge planes into the neighbours' mailboxes
+    after its last colour pass (peer_push_k), each descent pushes the coarse level's new b, and the
+    next consumer unpacks them -- no exchange.  The option must engage on every distributed level of
+    at least GHOST planes (the kernel name says so), and sweeps, V-cycles and the residual equal the
+    single-rank run bit for bit."""
+    import multigridanisotropicdiffusion_amd as M
+    from multigridanisotropicdiffusion_amd import distributed as D
+    T = synth.random_spd(SHAPE, seed=5)
+    x = synth.image(SHAPE, seed=6)
+    b = synth.image(SHAPE, seed=7)
+    sl = D.slabs(SHAPE, nranks)
+    global_nz = [SHAPE[0] >> l for l in range(8)]
+
+    def fn(r, s):
+        z0, z1 = (0, SHAPE[0]) if r is None else sl[r]
+        peer = []
+        if r is not None:
+            for l in range(s.num_levels):
+                nz = s.level_info(l)["shape"][0]
+                name = s.smooth_kernel_name(l)
+                if nz < global_nz[l] and nz >= 4:  # a rank slab of >= GHOST planes
+                    assert "gs_color_k" in name and "peer halo" in name, (l, name)
+                    peer.append(l)
+        s.upload(0, M.capi.X, x[z0:z1])
+        s.upload(0, M.capi.B, b[z0:z1])
+        s.smooth(0, 3)
+        a = s.download(0, M.capi.X)
+        for _ in range(3):
+            s.vcycle()
+        v = s.download(0, M.capi.X)
+        return a, v, s.residual(0), peer
+    kw = dict(options=M.capi.OPT_PEER_HALO, precision=M.FP32 if precision == "fp32" else M.FP64)
+    ref = _single(fn, T, **kw)
+    out = _multi(nranks, fn, T, **kw)
+    assert all(0 in o[3] and len(o[3]) >= 2 for o in out), [o[3] for o in out]
+    np.testing.assert_array_equal(np.concatenate([o[0] for o in out]), ref[0])
+    np.testing.assert_array_equal(np.concatenate([o[1] for o in out]), ref[1])
+    for o in out:
+        assert abs(o[2] - ref[2]) <= 1e-12 * ref[2]
