@@ -170,8 +170,11 @@ typedef struct mad_desc {
    the neighbours' mailboxes (device memory mapped across processes: hipIpc handles exchanged over the
    communicator) and counts its tiles in their counters while the rest of the sweep runs; the next
    consumer of the ghost planes waits for the neighbours' counters and copies the mailbox in (one small
-   launch) -- no exchange after the sweep.  Levels whose sweeps are not fused single launches keep the
-   exchange.  Identical results.  Setup-time option (mad_setup maps the windows, collectively). */
+   launch) -- no exchange after the sweep.  Levels swept colour by colour push their edge planes into the
+   mailboxes after the last colour pass instead (one small launch), and every descent into a distributed
+   level pushes the new coarse b the same way, so a rank's V-cycle keeps one collective, the all-gather
+   at the agglomeration level.  Identical results.  Setup-time option (mad_setup maps the windows,
+   collectively). */
 #define MAD_OPT_PEER_HALO 4u
 /* MAD_OPT_COARSE_NO_CHAIN: the block-plane direct solver (mad_coarse.hpp) without its chain
    matrices KL_i / KU_i even where they fit -- what it does by itself for one-plane blocks whose
