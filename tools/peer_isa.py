@@ -1,6 +1,6 @@
 """ISA evidence for the peer halo's memory ordering: compiles
 csrc/mad_solver.hip for gfx950 with --save-temps into a scratch directory and prints, for the
-producer (gs_fused3_k<float, FULL, ..., PEER = true, ...>, peer_ping_k) and the consumer
+producer (gs_fused3_k<float, FULL, ..., PEER = true, ...>, peer_push_k, peer_ping_k) and the consumer
 (peer_unpack_k, peer_pong_k), the instructions that carry the protocol: the mailbox stores and
 their cache-policy bits, the s_waitcnt before the counter atomic, the atomic's scope bits, and
 the system-scope acquire (load sc0 sc1 + buffer_inv sc0 sc1) before the mailbox reads.
@@ -34,7 +34,7 @@ def functions(asm):
     return out
 
 
-def excerpt(name, lines, limit=60):
+def excerpt(name, lines, limit=90):
     print(f"\n### {name}\n")
     body = [ln for ln in lines if ln.strip() and not ln.lstrip().startswith((";", ".loc", ".file", ".cfi"))]
     keep = [i for i, ln in enumerate(body) if KEEP.search(ln)]
@@ -68,6 +68,8 @@ def main():
          "_ZN3mad11gs_fused3_kIfLi3ELi64ELi32ELi1024ELi4ELi2ELb0ELb1ELb1ELb0E"),
         ("producer: the same sweep in the SMOOTHER layout (BREC 1, PEER 1)",
          "_ZN3mad11gs_fused3_kIfLi3ELi64ELi32ELi1024ELi4ELi2ELb1ELb1ELb0ELb0E"),
+        ("producer: per-colour levels' edge planes and the descents' coarse b (round 5) peer_push_k<float>",
+         "_ZN3mad11peer_push_kIfE"),
         ("setup self-test producer peer_ping_k<float>", "_ZN3mad11peer_ping_kIfE"),
         ("consumer peer_unpack_k", "_ZN3mad13peer_unpack_k"),
         ("setup self-test consumer peer_pong_k<float>", "_ZN3mad11peer_pong_kIfE"),
