@@ -912,10 +912,15 @@ class Solver final : public SolverBase {
     return MAD_FUSED_B_LDS && sizeof(T) == 4 && !L.brec && &L == &lv_[0];
   }
 
+  // fp32 full-tensor fused tiles: 64 x 32 in 1024 threads (A/B knob: 16 -> 64 x 16 in 512 threads,
+  // the halo-sensitivity probe of profiles/r05_tile_halo_ab.md)
+#ifndef MAD_FUSED_F32_TY
+#define MAD_FUSED_F32_TY 32
+#endif
   // tiles per plane and z-chunks of a whole-slab fused launch at level L
   void fused_shape(const LevelData<T>& L, int* tiles, int* nchunks) const {
     const FusedCfg fc = fused_cfg();
-    const int tx = 64, ty = (c_->kind == KFULL && sizeof(T) == 4) ? 32 : 16;
+    const int tx = 64, ty = (c_->kind == KFULL && sizeof(T) == 4) ? MAD_FUSED_F32_TY : 16;
     *tiles = ((L.g.nx + tx - 1) / tx) * ((L.g.ny + ty - 1) / ty);
     *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
   }
@@ -924,7 +929,7 @@ class Solver final : public SolverBase {
     const FusedCfg fc = fused_cfg();
     if (c_->kind == KFULL) {
       if constexpr (sizeof(T) == 4)
-        launch_fused<KFULL, 64, 32, 1024>(L, fc, part, zu);
+        launch_fused<KFULL, 64, MAD_FUSED_F32_TY, MAD_FUSED_F32_TY * 32>(L, fc, part, zu);
       else
         launch_fused<KFULL, 64, 16, 512>(L, fc, part, zu);
     } else if (c_->kind == KDIAG) {
@@ -953,8 +958,8 @@ class Solver final : public SolverBase {
       std::snprintf(buf, sizeof buf, "gs_color_k<%s, %d, %d>", tn, dim, kind);
       if (lv_[l].peer) return std::string(buf) + " [rank slab: peer halo, edge planes pushed after the last colour pass]";
     } else {
-      const int tx = 64, ty = (kind == KFULL && sizeof(T) == 4) ? 32 : 16;
-      const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : 1024;
+      const int tx = 64, ty = (kind == KFULL && sizeof(T) == 4) ? MAD_FUSED_F32_TY : 16;
+      const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : (kind == KFULL ? MAD_FUSED_F32_TY * 32 : 1024);
       const bool brec = lv_[l].brec;
       const LevelData<T>& L = lv_[l];
       // every template argument, as rocprofv3 prints the instantiation (BREC, PEER, BL, ZU last; the
