@@ -235,7 +235,7 @@ def test_solo_transport_times_one_rank():
 
 
 @pytest.mark.parametrize("cycle,gs_kernel,overlap", [(0, 0, 0), (2, 0, 0), (0, 3, 0), (0, 3, 1), (0, 3, 4),
-                                                     (2, 3, 4)])
+                                                     (2, 3, 4), (0, 0, 4)])
 def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     """The multi-rank V-cycle replays a captured hipGraph on RCCL / SOLO ranks (host bookkeeping
     of which ghost planes are current decides what the graph re-exchanges).  On the SOLO
@@ -245,7 +245,9 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     bit on every level's x and b; gs_kernel 3 puts the fused rank sweep into the graph, serial
     (the default), split (MAD_OPT_OVERLAP_RANK_SWEEP: a communication-stream branch) or with the
     peer halo (MAD_OPT_PEER_HALO: edge planes into the rank's own stand-in mailboxes, the unpack
-    launch waiting on its counters inside the graph)."""
+    launch waiting on its counters inside the graph); gs_kernel 0 with the peer halo pushes after the
+    per-colour sweeps and the descents (the single sweep in between flips level 0's mailbox parity,
+    which the graph is keyed on: it is re-captured)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     shape = (128, 64, 64)
@@ -276,7 +278,7 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
         np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")
 
 
-@pytest.mark.parametrize("cycle,gs_kernel,options", [(0, 0, 0), (0, 3, 0), (2, 3, 0), (0, 3, 4)])
+@pytest.mark.parametrize("cycle,gs_kernel,options", [(0, 0, 0), (0, 3, 0), (2, 3, 0), (0, 3, 4), (0, 0, 4)])
 def test_rccl_solo_equals_solo(cycle, gs_kernel, options):
     """mad_comm_init_rccl_solo moves SOLO's bytes through RCCL (a single-rank communicator, every
     grouped exchange ncclSend / ncclRecv pairs to itself, inside the captured V-cycle graph too):
