@@ -234,9 +234,10 @@ def test_solo_transport_times_one_rank():
         s.close()
 
 
-@pytest.mark.parametrize("cycle,gs_kernel,overlap", [(0, 0, 0), (2, 0, 0), (0, 3, 0), (0, 3, 1), (0, 3, 4),
-                                                     (2, 3, 4), (0, 0, 4)])
-def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
+@pytest.mark.parametrize("cycle,gs_kernel,overlap,nu", [(0, 0, 0, 2), (2, 0, 0, 2), (0, 3, 0, 2), (0, 3, 1, 2),
+                                                        (0, 3, 4, 2), (2, 3, 4, 2), (0, 0, 4, 2), (0, 0, 4, 1),
+                                                        (0, 0, 4, 3)])
+def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap, nu):
     """The multi-rank V-cycle replays a captured hipGraph on RCCL / SOLO ranks (host bookkeeping
     of which ghost planes are current decides what the graph re-exchanges).  On the SOLO
     transport (deterministic: every exchange a device copy) the same sequence -- sweeps,
@@ -247,7 +248,8 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     peer halo (MAD_OPT_PEER_HALO: edge planes into the rank's own stand-in mailboxes, the unpack
     launch waiting on its counters inside the graph); gs_kernel 0 with the peer halo pushes after the
     per-colour sweeps and the descents (the single sweep in between flips level 0's mailbox parity,
-    which the graph is keyed on: it is re-captured)."""
+    which the graph is keyed on: it is re-captured); nu = 1 / 3 sweeps per level (a cycle pushes 2 nu
+    batches per level, so a replay leaves the parity where the capture found it)."""
     import multigridanisotropicdiffusion_amd as M
     from multigridanisotropicdiffusion_amd import distributed as D
     shape = (128, 64, 64)
@@ -256,7 +258,8 @@ def test_solo_graph_replayed_vcycle_equals_eager(cycle, gs_kernel, overlap):
     base = {0: 0, 1: M.capi.OPT_OVERLAP_RANK_SWEEP, 4: M.capi.OPT_PEER_HALO}[overlap]
     for opt in (0, M.capi.OPT_EAGER_RANK_VCYCLE):
         s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, cycle=cycle, nranks=4, rank=2,
-                     global_shape=shape, min_slab_voxels=DEEP, options=opt | base, gs_kernel=gs_kernel)
+                     global_shape=shape, min_slab_voxels=DEEP, options=opt | base, gs_kernel=gs_kernel,
+                     iterations_per_grid=nu)
         s.comm_init_solo()
         s.synth_tensor(kind=0, seed=9)
         s.setup()
