@@ -1076,8 +1076,10 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
 // correction's update folded in, one GPU): every loaded u is u + (T) ue -- the fp32 cycle's
 // correction -- and the owned points' u + ue go to uo (a second buffer: neighbouring tiles still
 // read u); xe is then written by a separate fill, since those tiles also read ue.
-template <typename T, int KIND, int TX, int TY, bool BREC = false, typename TE = T>
-__global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const T* __restrict__ b,
+// TB: the storage type of b -- float where the refine rhs is an exactly-fp32 image (an 8/16-bit or fp32
+// input in its first time step): read as T, the same values in half the bytes.
+template <typename T, int KIND, int TX, int TY, bool BREC = false, typename TE = T, typename TB = T>
+__global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const TB* __restrict__ b,
                                                     T* __restrict__ r, const T* __restrict__ cf,
                                                     Geo g, Rat<T> rat, int zc, int ntx,
                                                     double* __restrict__ part,
@@ -1118,6 +1120,7 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
   const bool ok = i < nx && j < ny;
   const uint32_t rec_off = ok ? (uint32_t)(ty * sy + (tx & 1) * hx0 + (tx >> 1)) * (TS * RS) : 0u;
   const uint32_t pt_off = ok ? (uint32_t)(ty * sy + tx) * TS : 0u;
+  const uint32_t pt_off_b = ok ? (uint32_t)(ty * sy + tx) * (uint32_t)sizeof(TB) : 0u;
   const int64_t rbase = (int64_t)y0 * sy + (x0 >> 1), pbase = (int64_t)y0 * sy + x0;
   const int il = (ty + 1) * RX + (tx + 1);
   constexpr int oyp = RX, oym = -RX;  // x/y mirror images live in the ring
@@ -1146,7 +1149,7 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
   auto load_pt = [&](int m) {
     m = min(max(m, 0), g.nz - 1);
     buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + rbase) * RS), rec_off, raw);
-    if constexpr (!BREC) bv = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + pbase), pt_off, 0u);
+    if constexpr (!BREC) bv = (T)buf_load<TB>(buf_rsrc(b + (int64_t)m * sz + pbase), pt_off_b, 0u);
   };
 
   // prologue: planes z0-1, z0 in the ring, z0+1 in registers, point data of z0

@@ -406,6 +406,10 @@ class Solver final : public SolverBase {
       u64_ = r64alloc_[0] + margin + L0.ghost;
       b64_ = r64alloc_[1] + margin + L0.ghost;
       r64_ = r64alloc_[2] + margin + L0.ghost;
+      // b64 as fp32 for the time steps whose rhs is an exactly-fp32 image (residual64)
+      HIP_CHECK(big_alloc((void**)&b32alloc_, sizeof(float) * tot));
+      HIP_CHECK(hipMemsetAsync(b32alloc_, 0, sizeof(float) * tot, c->stream));
+      b32_ = b32alloc_ + margin + L0.ghost;
       const int64_t cgp = (dim == 3) ? GHOST : 0;
       const int64_t cplane = L0.g.sz * ncoef_;
       const int64_t ctot = (L0.g.nz + 2 * cgp) * cplane + 2 * margin * ncoef_;
@@ -1270,14 +1274,25 @@ class Solver final : public SolverBase {
       REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
       auto go = [&](auto K) {
         constexpr int KD = decltype(K)::value;
-        if (fold)
-          hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T>), dim3((unsigned)nparts), dim3(TX * TY),
-                             0, c_->stream, u64_, b64_, (double*)nullptr, cf64_, g, rat64_, zc, ntx, part_,
-                             L.b, (T*)nullptr, (const T*)L.x, r64_);
+        auto launch = [&](auto bptr) {
+          using TB = std::remove_const_t<std::remove_pointer_t<decltype(bptr)>>;
+          if (fold)
+            hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T, TB>), dim3((unsigned)nparts),
+                               dim3(TX * TY), 0, c_->stream, u64_, bptr, (double*)nullptr, cf64_, g, rat64_, zc,
+                               ntx, part_, L.b, (T*)nullptr, (const T*)L.x, r64_);
+          else
+            hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T, TB>), dim3((unsigned)nparts),
+                               dim3(TX * TY), 0, c_->stream, u64_, bptr, (double*)nullptr, cf64_, g, rat64_, zc,
+                               ntx, part_, L.b, L.x);
+        };
+#ifdef MAD_NO_B32_RHS  // A/B: always the fp64 rhs
+        launch((const double*)b64_);
+#else
+        if (b32_exact_)
+          launch((const float*)b32_);
         else
-          hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T>), dim3((unsigned)nparts), dim3(TX * TY),
-                             0, c_->stream, u64_, b64_, (double*)nullptr, cf64_, g, rat64_, zc, ntx, part_,
-                             L.b, L.x);
+          launch((const double*)b64_);
+#endif
       };
       refine_emitted_ = true;
       if (c_->kind == KFULL) go(std::integral_constant<int, KFULL>{});
@@ -1941,6 +1956,14 @@ class Solver final : public SolverBase {
       src = stage;
     }
     convert_to(src, in_dtype, b64_, N, c_->stream);
+    // an 8/16-bit or fp32 image is exactly an fp32 array: the first time step's fp64 residuals read
+    // its fp32 copy (the same values, 4 of the pass's 104 B per voxel saved)
+    b32_exact_ = in_dtype == MAD_U8 || in_dtype == MAD_I8 || in_dtype == MAD_U16 || in_dtype == MAD_I16 ||
+                 in_dtype == MAD_F32;
+    if (b32_exact_) {
+      hipLaunchKernelGGL((convert_k<double, float>), dim3(nb), dim3(256), 0, c_->stream, b64_, b32_, N);
+      HIP_CHECK(hipGetLastError());
+    }
     auto to_fp32_rhs = [&](const double* a) {  // level-0 b (fp32) <- a
       hipLaunchKernelGGL((convert_k<double, T>), dim3(nb), dim3(256), 0, c_->stream, a, L0.b, N);
       HIP_CHECK(hipGetLastError());
@@ -2063,6 +2086,7 @@ class Solver final : public SolverBase {
       c_->step_relres.push_back(relres);
       HIP_CHECK(hipMemcpyAsync(b64_, u64_, sizeof(double) * N, hipMemcpyDeviceToDevice,
                                c_->stream));  // MAD.hxx:248-261
+      b32_exact_ = false;  // the next step's rhs is the fp64 solution
     }
     HIP_CHECK(hipEventRecord(e1, c_->stream));
     // the last folded residual left x holding the last fp32 correction (the zero-iterate sweep
@@ -2191,6 +2215,9 @@ class Solver final : public SolverBase {
   double* r64alloc_[3] = {nullptr, nullptr, nullptr};
   double* u64_ = nullptr;
   double* b64_ = nullptr;
+  float* b32alloc_ = nullptr;  // b64_ as fp32 where it is exactly that (b32_exact_)
+  float* b32_ = nullptr;
+  bool b32_exact_ = false;
   double* r64_ = nullptr;
   double* cf64_alloc_ = nullptr;
   double* cf64_ = nullptr;
@@ -2257,6 +2284,9 @@ class Solver final : public SolverBase {
     if (cf64_alloc_) (void)hipFree(cf64_alloc_);
     cf64_alloc_ = nullptr;
     u64_ = b64_ = r64_ = cf64_ = nullptr;
+    if (b32alloc_) (void)hipFree(b32alloc_);
+    b32alloc_ = b32_ = nullptr;
+    b32_exact_ = false;
     if (part_) (void)hipFree(part_);
     if (scal_) (void)hipFree(scal_);
     if (hscal_) (void)hipHostFree(hscal_);

@@ -215,3 +215,27 @@ def test_zero_iterate_first_sweep_is_bitwise(M, gs_kernel):
     assert sa["last_relres"] <= 1e-10
     assert list(sa["step_cycles"]) == list(sb["step_cycles"])
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.uint8])
+def test_exact_fp32_rhs_is_bitwise(M, dtype):
+    """An 8/16-bit or fp32 input image is exactly an fp32 array, so in the first time step the
+    refine mode's fp64 residual reads b from an fp32 copy (4 instead of 8 B per voxel): the same
+    values, so the same bits as the fp64 rhs a float64 input of the same values takes -- iterate,
+    cycle counts and relres history, over two time steps (the second step's rhs is the fp64
+    solution again)."""
+    shape = (96, 80, 72)
+    T = synth.ved_form(shape)
+    img = synth.image(shape, seed=9) * 100
+    img = img.astype(dtype) if dtype != np.uint8 else np.clip(img + 128, 0, 255).astype(np.uint8)
+    outs = []
+    for src in (img, img.astype(np.float64)):
+        s = M.Solver(shape, time_step=0.4, tolerance=1e-10, precision=M.FP32_REFINE, number_of_steps=2)
+        s.set_tensor(T)
+        out, st = s.run(src, out_dtype=np.float64)
+        outs.append((out, st, [t[1] for t in s.cycle_trace()]))
+        s.close()
+    (a, sa, ta), (b, sb, tb) = outs
+    assert sa["last_relres"] <= 1e-10
+    assert list(sa["step_cycles"]) == list(sb["step_cycles"]) and ta == tb
+    assert np.array_equal(a, b)
