@@ -1412,6 +1412,7 @@ class Solver final : public SolverBase {
     sync_brec(l);
     b_changed(l + 1);
     T* zx = (zero_x && !handover) ? C.x : nullptr;
+    if (zx && C.x_peer_pending) peer_resolve(l + 1);  // (consumed before the zeros land on its ghost planes)
     // the kernel zeroes a rank slab's coarse x ghost planes too (the neighbours' zeros)
     if (zero_x && !handover) C.x_halo_ok = dist;
     // where the coarse planes go: the coarse level, or (hand-over) this rank's planes of it
@@ -2730,6 +2731,10 @@ class Solver final : public SolverBase {
   bool interp_ghosts(int l, bool add) {
     LevelData<T>& F = lv_[l];
     if (!c_->comm.active() || !c_->geom[l].distributed || c_->dim != 3) return false;
+    // a peer batch still in flight for x (the previous time step's last sweep, when FMG's
+    // interpolation is the level's first use of x) is taken in first: it must not land on the
+    // ghost planes this interpolation writes, and x += P e needs it there
+    if (F.x_peer_pending) peer_resolve(l);
     if (add && !F.x_halo_ok) return false;
     wait_all_pending();  // the ghost planes may still be arriving
     return true;

@@ -169,15 +169,21 @@ def test_cycle_trace_matches_oracle_history(M, oracle_mod):
     assert all(b2 >= a2 for a2, b2 in zip(secs, secs[1:])) and secs[0] > 0
 
 
-def test_refine_rank_slabs_match_single(M):
+@pytest.mark.parametrize("variant", ["f64_input", "f32_input_peer_fmg"])
+def test_refine_rank_slabs_match_single(M, variant):
     """Refined runs on z-slabs (in-process transport, 2 ranks): the fp64 residual's halo and
-    norm allreduce; same cycle counts and result within 1e-12 of the single-rank run."""
+    norm allreduce; same cycle counts and result within 1e-12 of the single-rank run.  Second
+    variant: an fp32 input (the exactly-fp32 rhs in the first step) in CycleType FMG with the
+    peer halo on every distributed level (per-colour pushes, the descents' b pushes)."""
     from multigridanisotropicdiffusion_amd import distributed as D
     shape = (64, 48, 40)
     T = synth.ved_form(shape)
     img = synth.image(shape, seed=5) * 100
     sl = D.slabs(shape, 2)
     kw = dict(time_step=0.4, tolerance=1e-10, precision=M.FP32_REFINE, number_of_steps=2)
+    if variant != "f64_input":
+        img = img.astype(np.float32)
+        kw.update(cycle=M.FMG, options=M.capi.OPT_PEER_HALO)
     s = M.Solver(shape, **kw)
     s.set_tensor(T)
     ref, rst = s.run(img, out_dtype=np.float64)
