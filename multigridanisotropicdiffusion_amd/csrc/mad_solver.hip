@@ -320,6 +320,9 @@ struct LevelData {
   // b of a distributed coarse level: the descent pushes its edge planes (one buffer, mailboxes
   // [4 + side], counters [8 + side]); the first sweep takes them in
   bool b_peer_pending = false;
+  // x is zero but was not written (the V-cycle descent left it to the level's first sweep, which
+  // takes its planes as zeros: gs_fused3_k ZU); any other write of x clears it
+  bool x_zero_lazy = false;
 };
 // z-depth of a rank slab's boundary chunks (>= GHOST; 4 measured 0.231 vs 0.228 ms per 8-rank
 // sweep, profiles/r02_slab_tiles.log)
@@ -760,6 +763,7 @@ class Solver final : public SolverBase {
   void x_changed(int l) {
     if (lv_[l].x_peer_pending) peer_resolve(l);
     lv_[l].x_halo_ok = false;
+    lv_[l].x_zero_lazy = false;
   }
 
   // target grid size of the z-marching transfer kernels
@@ -1073,9 +1077,11 @@ class Solver final : public SolverBase {
                                std::is_same<T, double>::value, c_->comm_stream);
       HIP_CHECK(hipEventRecord(L.ev_halo, c_->comm_stream));
     } else if (!overlap) {
-      // the first sweep of a refine correction cycle: x is zero by construction (run_refine)
-      const bool zu = zero_x0_ && &L == &lv_[0];
+      // the first sweep of a refine correction cycle (x zero by construction, run_refine), or of a
+      // coarse level whose descent left its zero x unwritten (x_zero_lazy)
+      const bool zu = (zero_x0_ && &L == &lv_[0]) || L.x_zero_lazy;
       zero_x0_ = false;
+      L.x_zero_lazy = false;
       launch_fused_part(L, 0, zu);
     } else {
       launch_fused_part(L, 1);
@@ -1239,6 +1245,19 @@ class Solver final : public SolverBase {
   // only where that sweep is the first thing of the cycle to touch x: a fused fp32 whole-slab
   // sweep at level 0 of a multi-level V-cycle, with pre-smoothing, on one GPU
   bool zero_x0_ = false;
+  // a V-cycle descent into level l (>= 1) may leave x[l] unwritten: its first sweep is a fused fp32
+  // whole-slab one-GPU sweep (the ZU instance) and nothing reads x[l] before it (pre-smoothing, not
+  // verbose, not the coarsest)
+  bool lazy_zero_ok(int l) const {
+#ifdef MAD_NO_LAZY_ZERO
+    return false;
+#else
+    const auto& d = c_->d;
+    return sizeof(T) == 4 && l >= 1 && l < c_->nlev - 1 && !c_->comm.active() && !d.verbose &&
+           d.iterations_per_grid >= 1 && use_fused(l) && d.gs_kernel != 4 && !lv_[l].brec &&
+           c_->dim == 3;
+#endif
+  }
   bool zero_sweep_ok() const {
 #ifdef MAD_NO_ZERO_SWEEP
     return false;
@@ -1413,6 +1432,10 @@ class Solver final : public SolverBase {
     b_changed(l + 1);
     T* zx = (zero_x && !handover) ? C.x : nullptr;
     if (zx && C.x_peer_pending) peer_resolve(l + 1);  // (consumed before the zeros land on its ghost planes)
+    if (zx && lazy_zero_ok(l + 1)) {  // the coarse level's first sweep takes x as zero without loading it
+      zx = nullptr;
+      C.x_zero_lazy = true;
+    }
     // the kernel zeroes a rank slab's coarse x ghost planes too (the neighbours' zeros)
     if (zero_x && !handover) C.x_halo_ok = dist;
     // where the coarse planes go: the coarse level, or (hand-over) this rank's planes of it
