@@ -80,8 +80,12 @@ typedef enum mad_precision {
 #define MAD_FP32_TOLERANCE_FLOOR 1e-6
 /* MAD_FP32_REFINE V-cycle / FMG solves run their first cycles in plain fp32 (fp32 iterate, fp32
    residual norm) until relres drops below this, far above fp32's ~1e-7 floor; the iterate then moves
-   to fp64 and the defect correction continues (SMOOTHER runs refine from the first sweep) */
+   to fp64 and the defect correction continues (SMOOTHER runs refine from the first sweep).  The
+   fp32 phase also ends when a cycle reduces relres by less than 1 / MAD_REFINE_FP32_MIN_RATE (fp32's
+   floor rises with the conditioning: large time steps, strong anisotropy) and one cycle before
+   MaxCycles, so the defect correction always gets a turn (MaxCycles 1 refines from the start) */
 #define MAD_REFINE_SWITCH_RELRES 1e-5
+#define MAD_REFINE_FP32_MIN_RATE 0.5
 /* defaults of mad_desc.min_slab_planes / min_slab_voxels (measured: profiles/r03_agglomeration.md,
    profiles/r03_rank_serial_ab.md) */
 #define MAD_MIN_SLAB_PLANES 4
@@ -181,6 +185,16 @@ typedef struct mad_desc {
    KL / KU would take more than half the free device memory (e.g. a 512 x 512 x 8 whole-grid
    solve: 69 instead of 206 GB); one more launch per chain step, the same result to fp64 rounding */
 #define MAD_OPT_COARSE_NO_CHAIN 8u
+/* MAD_OPT_BENCHMARK_TRACE: mad_get_cycle_trace returns the reference's -DBENCHMARK history instead of
+   one entry per cycle -- in VCYCLE / FMG, level 0's relative residual after every pre-smoothing
+   sweep, after the coarse-grid correction and after every post-smoothing sweep of every level-0
+   V-cycle, FMG's included (MAD.hxx:401-409, 450-458, 477-485: 2 nu + 1 entries per V-cycle), in
+   SMOOTHER after every sweep (:222-227); seconds since the time step's start (the reference resets
+   m_Time per step, :158-163).  V-cycles then run eagerly with a residual norm read back after every
+   level-0 sweep (a measurement mode, as the reference's); off by default.  In MAD_FP32_REFINE the
+   correction cycles' entries are the fp32 residual of the correction equation over the step's
+   ||b||, i.e. the relres of the updated iterate to fp32 rounding. */
+#define MAD_OPT_BENCHMARK_TRACE 16u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */
@@ -238,12 +252,14 @@ int mad_run_device(mad_ctx *ctx, const void *dev_in, int32_t in_dtype, void *dev
                    int32_t out_dtype, mad_stats *stats);
 /* per-time-step history of the last run */
 int mad_get_step_stats(const mad_ctx *ctx, uint32_t step, uint32_t *cycles, double *relres);
-/* Convergence history of the last run, one entry per cycle (V-cycle / FMG cycle / smoother
- * sweep): the time step it belongs to, the relative residual ||b - A x|| / ||b|| after it and
- * the seconds since the run started (host wall clock, the norm is read back every cycle).
- * The reference writes the same pairs to benchmark.txt under -DBENCHMARK
- * (MAD.hxx:147-151, 222-227).  Copies min(cap, total) entries (any pointer may be NULL);
- * *count = total entries of the run. */
+/* Convergence history of the last run.  Default: one entry per cycle (V-cycle / FMG cycle /
+ * smoother sweep): the time step it belongs to, the relative residual ||b - A x|| / ||b|| after it
+ * and the seconds since the run started (host wall clock, the norm is read back every cycle).
+ * This is the reference's -DBENCHMARK benchmark.txt (MAD.hxx:147-151, 222-227) only in SMOOTHER
+ * mode; in VCYCLE / FMG the reference writes 2 nu + 1 entries per level-0 V-cycle (after every
+ * sweep and after the correction, :401-409, 450-458, 477-485) and nothing per cycle -- that
+ * history, with the reference's per-step clock, is what mad_desc.options MAD_OPT_BENCHMARK_TRACE
+ * records.  Copies min(cap, total) entries (any pointer may be NULL); *count = total entries. */
 int mad_get_cycle_trace(const mad_ctx *ctx, uint32_t cap, uint32_t *step, double *relres,
                         double *seconds, uint32_t *count);
 

@@ -34,6 +34,7 @@ OPT_EAGER_RANK_VCYCLE = 1
 OPT_OVERLAP_RANK_SWEEP = 2
 OPT_PEER_HALO = 4
 OPT_COARSE_NO_CHAIN = 8
+OPT_BENCHMARK_TRACE = 16  # the reference's -DBENCHMARK history in mad_get_cycle_trace (include/mad.h)
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (

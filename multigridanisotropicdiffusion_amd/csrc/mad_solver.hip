@@ -215,13 +215,23 @@ struct mad_ctx {
   std::unique_ptr<SolverBase> solver;
   std::vector<uint32_t> step_cycles;
   std::vector<double> step_relres;
-  // per-cycle convergence history of the last run (mad_get_cycle_trace; the reference's
-  // BENCHMARK trace, MAD.hxx:147-151, 222-227)
+  // convergence history of the last run (mad_get_cycle_trace): one entry per cycle, or with
+  // MAD_OPT_BENCHMARK_TRACE the reference's -DBENCHMARK entries (MAD.hxx:147-151, 222-227,
+  // 401-409, 450-458, 477-485: level 0 after every sweep and after the coarse-grid correction,
+  // seconds since the time step's start)
   struct TracePoint {
     uint32_t step;
     double relres, seconds;
   };
   std::vector<TracePoint> trace;
+  bool bench_trace() const { return (d.options & MAD_OPT_BENCHMARK_TRACE) != 0; }
+  bool trace_active = false;  // inside mad_run (kernel-API V-cycles record nothing)
+  uint32_t trace_step = 0;
+  double trace_rhs = 1.0;  // ||b|| of the time step (the relres denominator)
+  std::chrono::steady_clock::time_point trace_t0{};  // the run's start / the step's (benchmark form)
+  void trace_push(double rr) {
+    trace.push_back({trace_step, rr, std::chrono::duration<double>(std::chrono::steady_clock::now() - trace_t0).count()});
+  }
   double setup_ms = 0.0;
   Comm comm;
   ~mad_ctx();
@@ -280,6 +290,8 @@ struct LevelData {
   T* t = nullptr;  // WJ ping-pong / scratch
   T* cf = nullptr;        // field 0, plane 0 (ghost planes precede it on rank slabs)
   T* cf_alloc = nullptr;
+  char* pool = nullptr;   // the one allocation alloc[] / cf_alloc are carved from (mad_alloc.hpp Placement)
+  void* pool_own[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // arrays placed outside it
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -364,9 +376,40 @@ class Solver final : public SolverBase {
       // up to a tile halo outside the outermost (ghost) plane
       const int64_t margin = margin_elems(L.g);
       const int64_t tot = L.g.N + 2 * (L.ghost + margin);
-      for (int a = 0; a < 4; ++a) {
-        level_alloc((void**)&L.alloc[a], sizeof(T) * tot);
-        HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
+      // (record stride first: a pooled level 0 sizes its record array with it)
+      bool brec_on = c->d.cycle == MAD_SMOOTHER;
+      if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
+      L.brec = (dim == 3 && l == 0 && brec_on);
+      L.g.rs = ncoef_ + (L.brec ? 1 : 0);
+      const int64_t cplane = L.g.sz * L.g.rs;
+      const int64_t cgp = (dim == 3) ? GHOST : 0;
+      const int64_t cmargin = margin * L.g.rs;
+      const int64_t ctot = (L.g.nz + 2 * cgp) * cplane + 2 * cmargin;
+      const Placement place = (l == 0 && dim == 3) ? level0_placement() : Placement{};
+      if (place.on) {
+        const size_t bytes[5] = {sizeof(T) * tot, sizeof(T) * tot, sizeof(T) * tot, sizeof(T) * tot,
+                                 sizeof(T) * ctot};
+        size_t at[5];
+        const size_t pool = place_offsets(place, bytes, at);
+        HIP_CHECK(contiguous_alloc((void**)&L.pool, pool));
+        HIP_CHECK(hipMemsetAsync(L.pool, 0, pool, c->stream));
+        T** dst[5] = {&L.alloc[0], &L.alloc[1], &L.alloc[2], &L.alloc[3], &L.cf_alloc};
+        for (int a = 0; a < 5; ++a) {
+          if (place.own[a]) {
+            level_alloc((void**)dst[a], bytes[a]);
+            HIP_CHECK(hipMemsetAsync(*dst[a], 0, bytes[a], c->stream));
+            L.pool_own[a] = *dst[a];
+          } else {
+            *dst[a] = (T*)(L.pool + at[a]);
+          }
+        }
+      } else {
+        for (int a = 0; a < 4; ++a) {
+          level_alloc((void**)&L.alloc[a], sizeof(T) * tot);
+          HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
+        }
+        level_alloc((void**)&L.cf_alloc, sizeof(T) * ctot);
+        HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
       }
       L.x = L.alloc[0] + margin + L.ghost;
       L.b = L.alloc[1] + margin + L.ghost;
@@ -383,16 +426,7 @@ class Solver final : public SolverBase {
       // every time step after ~2 cycles (~12 level-0 record passes), where the 2.2 ms
       // scatter of b into the 40-B records (partial-line writes, 512^3) costs more than
       // it saves (VED diffusion 126 -> 116.5 ms without it, profiles/r01_brec_ab.log).
-      bool brec_on = c->d.cycle == MAD_SMOOTHER;
-      if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
-      L.brec = (dim == 3 && l == 0 && brec_on);
-      L.g.rs = ncoef_ + (L.brec ? 1 : 0);
-      const int64_t cplane = L.g.sz * L.g.rs;
-      const int64_t cgp = (dim == 3) ? GHOST : 0;
-      const int64_t cmargin = margin * L.g.rs;
-      const int64_t ctot = (L.g.nz + 2 * cgp) * cplane + 2 * cmargin;
-      level_alloc((void**)&L.cf_alloc, sizeof(T) * ctot);
-      HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
+      // (L.brec / L.g.rs are set above, before the allocation)
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
@@ -1564,14 +1598,15 @@ class Solver final : public SolverBase {
     const int nl = c_->nlev;
     if (l == nl - 1) {  // MAD.hxx:356-371
       coarse_solve();
-      if (c_->d.verbose) verbose_line(l, -1, "direct solver");
+      if (c_->d.verbose) (void)verbose_line(l, -1, "direct solver");
       return;
     }
     const unsigned nu = c_->d.iterations_per_grid;
-    if (c_->d.verbose) {
+    const bool bt = l == 0 && c_->bench_trace() && c_->trace_active;  // MAD.hxx:401-409
+    if (c_->d.verbose || bt) {
       for (unsigned n = 0; n < nu; ++n) {
         smooth(l, 1);
-        verbose_line(l, (int)n + 1, nullptr);
+        per_sweep_line(l, (int)n + 1, nullptr, bt);
       }
     } else {
       smooth(l, nu);  // MAD.hxx:384-411
@@ -1583,11 +1618,11 @@ class Solver final : public SolverBase {
     }
     vcycle_rec(l + 1);        // MAD.hxx:418-420
     interpolate_up(l, true);  // MAD.hxx:422-435
-    if (c_->d.verbose) verbose_line(l, 0, "initial");
-    if (c_->d.verbose) {
+    if (c_->d.verbose || bt) per_sweep_line(l, 0, "initial", bt);  // MAD.hxx:450-458
+    if (c_->d.verbose || bt) {
       for (unsigned n = 0; n < nu; ++n) {
         smooth(l, 1);
-        verbose_line(l, (int)n + 1, nullptr);
+        per_sweep_line(l, (int)n + 1, nullptr, bt);  // MAD.hxx:477-485
       }
     } else {
       smooth(l, nu);  // MAD.hxx:460-487
@@ -1691,7 +1726,7 @@ class Solver final : public SolverBase {
 
   void vcycle_fast() {
     const bool ranks = c_->comm.active();
-    if (c_->d.verbose || vgraph_failed_ || (ranks && !vgraph_ranks_ok()) ||
+    if (c_->d.verbose || c_->bench_trace() || vgraph_failed_ || (ranks && !vgraph_ranks_ok()) ||
         (ranks && vcycles_eager_ < 1)) {
       if (ranks) ++vcycles_eager_;
       vcycle_rec(0);
@@ -1819,15 +1854,29 @@ class Solver final : public SolverBase {
 
   void fmg() override { fmg_rec(0); }
 
-  void verbose_line(int l, int it, const char* what) {
-    LevelData<T>& L = lv_[l];
+  // the verbose line and / or the level-0 benchmark-trace entry of one point of a V-cycle
+  void per_sweep_line(int l, int it, const char* what, bool bench) {
+    if (!c_->d.verbose) {  // benchmark trace only: level 0's relres against the time step's ||b||
+      const double rn = residual(l, true);
+      c_->trace_push(c_->trace_rhs > 0.0 ? rn / c_->trace_rhs : rn);
+      return;
+    }
+    const double rel = verbose_line(l, it, what);
+    if (bench) {
+      // the verbose line's ||b|| is level 0's b: the time step's rhs except in the refine mode's
+      // correction cycles (b = the fp64 residual), whose relres is taken against the step's rhs
+      const double rn = rel * norm(l, MAD_B);
+      c_->trace_push(c_->trace_rhs > 0.0 ? rn / c_->trace_rhs : rn);
+    }
+  }
+
+  double verbose_line(int l, int it, const char* what) {
     // rhsNorm (MAD.hxx:352) and the residual norm of the current iterate
     const double bn = norm(l, MAD_B);
     // keep r intact: the residual kernel writes r, which at this point is scratch
     const double rn = residual(l, true);
     const double rel = rn / bn;
-    (void)L;
-    if (c_->comm.rank() != 0) return;
+    if (c_->comm.rank() != 0) return rel;
     std::string ind(l + 1, ' ');
     if (what && std::strcmp(what, "direct solver") == 0)
       std::printf("%sLevel %d, direct solver: relative residual = %g\n", ind.c_str(), l, rel);
@@ -1836,6 +1885,7 @@ class Solver final : public SolverBase {
     else
       std::printf("%sLevel %d, iteration %d: relative residual = %g\n", ind.c_str(), l, it, rel);
     std::fflush(stdout);
+    return rel;
   }
 
   // ------------------------------------------------------------- filter
@@ -1865,9 +1915,16 @@ class Solver final : public SolverBase {
     c_->step_cycles.clear();
     c_->step_relres.clear();
     c_->trace.clear();
-    const auto t_run = std::chrono::steady_clock::now();
+    // per-cycle entries (seconds since the run's start); with MAD_OPT_BENCHMARK_TRACE the V-cycle
+    // records level 0's entries itself (per_sweep_line) and only SMOOTHER sweeps are recorded here,
+    // with seconds since the time step's start (the reference's m_Time, MAD.hxx:158-163)
+    const bool bt = c_->bench_trace();
+    c_->trace_active = true;
+    c_->trace_t0 = std::chrono::steady_clock::now();
     auto trace = [&](unsigned step, double rr) {
-      c_->trace.push_back({step, rr, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count()});
+      if (bt && d.cycle != MAD_SMOOTHER) return;
+      c_->trace_step = step;
+      c_->trace_push(rr);
     };
     bool stalled_any = false;
     unsigned total = 0;
@@ -1875,6 +1932,11 @@ class Solver final : public SolverBase {
     for (unsigned step = 0; step < d.number_of_steps; ++step) {  // MAD.hxx:158
       if (d.verbose && d.number_of_steps > 1 && c_->comm.rank() == 0)
         std::printf("\n------------ Time step n. %u / %u------------\n", step + 1, d.number_of_steps);
+      if (bt) {
+        c_->trace_t0 = std::chrono::steady_clock::now();
+        c_->trace_step = step;
+        c_->trace_rhs = norm(0, MAD_B);  // the rhsNorm of the step's level-0 V-cycles (MAD.hxx:352)
+      }
       if (d.cycle == MAD_FMG) {
         if (d.verbose && c_->comm.rank() == 0) std::printf("|--- Full Multigrid Cycle ---|\n");
         fmg_rec(0);  // MAD.hxx:170-176
@@ -1929,6 +1991,7 @@ class Solver final : public SolverBase {
                                c_->stream));  // MAD.hxx:248-261
       L0.b_halo_ok = L0.brec_ok = false;
     }
+    c_->trace_active = false;
     HIP_CHECK(hipEventRecord(e1, c_->stream));
     // cast solution -> output type (MAD.hxx:266-289)
     void* dst = out;
@@ -2000,9 +2063,16 @@ class Solver final : public SolverBase {
     c_->step_cycles.clear();
     c_->step_relres.clear();
     c_->trace.clear();
-    const auto t_run = std::chrono::steady_clock::now();
+    // per-cycle entries (seconds since the run's start); with MAD_OPT_BENCHMARK_TRACE the V-cycle
+    // records level 0's entries itself (per_sweep_line) and only SMOOTHER sweeps are recorded here,
+    // with seconds since the time step's start (the reference's m_Time, MAD.hxx:158-163)
+    const bool bt = c_->bench_trace();
+    c_->trace_active = true;
+    c_->trace_t0 = std::chrono::steady_clock::now();
     auto trace = [&](unsigned step, double rr) {
-      c_->trace.push_back({step, rr, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count()});
+      if (bt && d.cycle != MAD_SMOOTHER) return;
+      c_->trace_step = step;
+      c_->trace_push(rr);
     };
     bool stalled_any = false;
     unsigned total = 0;
@@ -2018,8 +2088,14 @@ class Solver final : public SolverBase {
 #ifdef MAD_NO_REFINE_FP32_PHASE  // A/B: refine from the first cycle
       const bool fp32_phase = false;
 #else
-      const bool fp32_phase = d.cycle != MAD_SMOOTHER;
+      // (at least two cycles allowed: the fp32 phase always leaves the defect correction a turn)
+      const bool fp32_phase = d.cycle != MAD_SMOOTHER && d.max_cycles >= 2;
 #endif
+      if (bt) {
+        c_->trace_t0 = std::chrono::steady_clock::now();
+        c_->trace_step = step;
+        c_->trace_rhs = norm64(b64_);  // MAD.hxx:204 / 352
+      }
       if (d.cycle == MAD_FMG) {
         if (d.verbose && c_->comm.rank() == 0) std::printf("|--- Full Multigrid Cycle ---|\n");
         to_fp32_rhs(b64_);
@@ -2055,7 +2131,11 @@ class Solver final : public SolverBase {
           ++it;
           trace(step, relres);
           hist.push_back(relres);
-        } while (relres > std::max(d.tolerance, MAD_REFINE_SWITCH_RELRES) && it < d.max_cycles);
+          // plain fp32 levels off at a floor that grows with the conditioning (large time steps,
+          // strong anisotropy): once a cycle reduces relres by less than 2x, the fp64 defect
+          // correction takes over, and the phase ends one cycle before MaxCycles so it always does
+          if (hist.size() >= 2 && relres > MAD_REFINE_FP32_MIN_RATE * hist[hist.size() - 2]) break;
+        } while (relres > std::max(d.tolerance, MAD_REFINE_SWITCH_RELRES) && it + 1 < d.max_cycles);
         hipLaunchKernelGGL((convert_k<T, double>), dim3(nb), dim3(256), 0, c_->stream, L0.x, u64_, N);
         HIP_CHECK(hipGetLastError());
       }
@@ -2066,7 +2146,8 @@ class Solver final : public SolverBase {
         relres = (rhsNorm > 0.0) ? resNorm / rhsNorm : resNorm;
         if (!hist.empty()) {
           hist.back() = relres;
-          c_->trace.back().relres = relres;
+          // (the per-cycle entry; with the benchmark trace the last post-smoothing sweep's)
+          if (!c_->trace.empty()) c_->trace.back().relres = relres;
         }
       }
       if (!fp32_phase || (relres > d.tolerance && it < d.max_cycles)) do {  // MAD.hxx:207-246
@@ -2094,6 +2175,8 @@ class Solver final : public SolverBase {
           std::printf("Smoother iteration n. %u: relative residual = %g\n", it + 1, relres);
         ++it;
         trace(step, relres);
+        // benchmark trace: the last post-smoothing entry is the updated iterate's, now in fp64
+        if (bt && d.cycle != MAD_SMOOTHER && !c_->trace.empty()) c_->trace.back().relres = relres;
         hist.push_back(relres);
         // fallback only: the fp64 residual keeps falling where plain fp32 stalls
         if (d.stall_guard && hist.size() > window && relres < 1e-3 && relres > d.tolerance) {
@@ -2112,6 +2195,7 @@ class Solver final : public SolverBase {
                                c_->stream));  // MAD.hxx:248-261
       b32_exact_ = false;  // the next step's rhs is the fp64 solution
     }
+    c_->trace_active = false;
     HIP_CHECK(hipEventRecord(e1, c_->stream));
     // the last folded residual left x holding the last fp32 correction (the zero-iterate sweep
     // never needed it cleared): leave level-0 x = 0, as the unfolded pass does, for direct
@@ -2298,9 +2382,15 @@ class Solver final : public SolverBase {
       Comm::close_window(L.win_lo, L.win_ipc);
       Comm::close_window(L.win_hi, L.win_ipc);
       if (L.win) (void)hipFree(L.win);
-      for (auto& a : L.alloc)
-        if (a) (void)hipFree(a);
-      if (L.cf_alloc) (void)hipFree(L.cf_alloc);
+      if (L.pool) {
+        (void)hipFree(L.pool);
+        for (auto& a : L.pool_own)
+          if (a) (void)hipFree(a);
+      } else {
+        for (auto& a : L.alloc)
+          if (a) (void)hipFree(a);
+        if (L.cf_alloc) (void)hipFree(L.cf_alloc);
+      }
     }
     lv_.clear();
     for (auto& a : r64alloc_)

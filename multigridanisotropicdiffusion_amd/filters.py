@@ -81,7 +81,11 @@ class MultigridAnisotropicDiffusionImageFilter:
     VCYCLE, FMG, SMOOTHER = C.VCYCLE, C.FMG, C.SMOOTHER
 
     def __init__(self, smoother=MultigridGaussSeidelSmoother, output_dtype=np.float32,
-                 precision=C.PRECISION_AUTO, device=-1):
+                 precision=C.PRECISION_AUTO, device=-1, benchmark=False):
+        # benchmark: the reference's -DBENCHMARK build (.hxx:145-151): Update() records the
+        # relres / seconds history the reference writes to benchmark.txt (GetBenchmarkOutput)
+        self._benchmark = bool(benchmark)
+        self.benchmark_trace = None
         self._smoother = smoother
         self._output_dtype = np.dtype(output_dtype)
         self._precision = precision
@@ -136,6 +140,13 @@ class MultigridAnisotropicDiffusionImageFilter:
     def GetOutput(self):
         return self._output
 
+    def GetBenchmarkOutput(self):
+        """The lines the reference's -DBENCHMARK build writes to benchmark.txt, "relres_seconds"
+        (.hxx:222-227, 401-409, 450-458, 477-485); needs benchmark=True."""
+        if self.benchmark_trace is None:
+            raise RuntimeError("construct with benchmark=True and call Update first")
+        return [f"{rr:g}_{sec:g}" for _, rr, sec in self.benchmark_trace]
+
     def Update(self):
         """GenerateData (.hxx:104-297) on the GPU."""
         if self._input is None or self._tensor is None:
@@ -147,10 +158,13 @@ class MultigridAnisotropicDiffusionImageFilter:
                    smoother=smoother.smoother_id, iterations_per_grid=self._iterations_per_grid,
                    max_cycles=self._max_cycles, number_of_steps=self._number_of_steps,
                    tolerance=self._tolerance, omega=weight, verbose=self._verbose,
-                   precision=self._precision, device=self._device)
+                   precision=self._precision, device=self._device,
+                   options=C.OPT_BENCHMARK_TRACE if self._benchmark else 0)
         try:
             s.set_tensor(self._tensor)
             out, stats = s.run(img.array, out_dtype=self._output_dtype)
+            if self._benchmark:
+                self.benchmark_trace = s.cycle_trace()
         finally:
             s.close()
         self.stats = stats

@@ -289,9 +289,13 @@ class Solver:
         return out, stats
 
     def cycle_trace(self):
-        """Per-cycle history of the last run (mad_get_cycle_trace): list of (time step,
-        relres after the cycle, seconds since the run started) -- the reference's BENCHMARK
-        trace (itkMultigridAnisotropicDiffusionImageFilter.hxx:147-151, 222-227)."""
+        """Convergence history of the last run (mad_get_cycle_trace): list of (time step,
+        relres, seconds).  Default: one entry per cycle, seconds since the run started.  With
+        options=capi.OPT_BENCHMARK_TRACE: the reference's -DBENCHMARK history -- level 0 after
+        every sweep and after the coarse-grid correction of every level-0 V-cycle (2 nu + 1 per
+        cycle; SMOOTHER: every sweep), seconds since the time step started
+        (itkMultigridAnisotropicDiffusionImageFilter.hxx:147-151, 222-227, 401-409, 450-458,
+        477-485)."""
         n = ctypes.c_uint32()
         self._check(self._L.mad_get_cycle_trace(self._ctx, 0, None, None, None, ctypes.byref(n)))
         k = n.value

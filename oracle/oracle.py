@@ -225,6 +225,22 @@ class Oracle:
         lib().ora_fmg(self._c, ctypes.byref(p), _dp(self._in(b)), _dp(out))
         return out
 
+    def run_benchmark(self, image, **kw):
+        """Whole filter with the verbose trace; returns (output, cycles, relres, history) where
+        history is the reference's -DBENCHMARK relres sequence of a V-cycle / FMG run: the
+        level-0 entries of the trace, i.e. after every level-0 sweep and after the level-0
+        coarse-grid correction (MAD.hxx:401-409, 450-458, 477-485)."""
+        L = lib()
+        L.ora_take_trace(self._c, 0, None, None, None)
+        out, cyc, rr = self.run(image, verbose=1, **kw)
+        cap = 1 << 20
+        lv = (ctypes.c_int * cap)()
+        it = (ctypes.c_int * cap)()
+        rel = (ctypes.c_double * cap)()
+        n = L.ora_take_trace(self._c, cap, lv, it, rel)
+        assert n <= cap
+        return out, cyc, rr, [rel[i] for i in range(n) if lv[i] == 0 and it[i] >= 0]
+
     def run(self, image, **kw):
         """Whole filter (GenerateData) in fp64; returns (output, cycles, relres)."""
         p = params(**kw)

@@ -57,8 +57,32 @@ def order(n, free=False, prealloc=0):
               flush=True)
 
 
+def places(specs, reps):
+    """round 6: level 0's arrays carved from one contiguous block at the given relative offsets
+    (MAD_LEVEL0_PLACE, csrc/mad_alloc.hpp Placement; "sep" = separate allocations), fresh process
+    each, the specs alternated `reps` times"""
+    for rep in range(reps):
+        for spec in specs:
+            env = dict(os.environ)
+            env.pop("MAD_LEVEL0_PLACE", None)
+            if spec != "sep":
+                env["MAD_LEVEL0_PLACE"] = spec
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", "0"], capture_output=True,
+                               text=True, timeout=120, env=env)
+            out = r.stdout.strip()
+            kern = json.loads(out)["kernel_ms"] if r.returncode == 0 and out else None
+            notes = [ln for ln in r.stderr.splitlines() if ln.startswith("[mad]")]
+            print(json.dumps({"rep": rep, "place": spec, "kernel_ms": kern, "notes": notes}) if kern else
+                  f"{spec}: rc {r.returncode} {r.stderr[-400:]}", flush=True)
+            if r.returncode != 0:
+                return 1
+    return 0
+
+
 def main():
     a = sys.argv[1:]
+    if a and a[0] == "--places":
+        return places(a[2:], int(a[1]))
     if a and a[0] == "--one":
         return one(int(a[1]))
     if a and a[0] == "--order":
