@@ -183,7 +183,9 @@ typedef struct mad_desc {
 /* MAD_OPT_COARSE_NO_CHAIN: the block-plane direct solver (mad_coarse.hpp) without its chain
    matrices KL_i / KU_i even where they fit -- what it does by itself for one-plane blocks whose
    KL / KU would take more than half the free device memory (e.g. a 512 x 512 x 8 whole-grid
-   solve: 69 instead of 206 GB); one more launch per chain step, the same result to fp64 rounding */
+   solve: 69 instead of 206 GB); one more launch per chain step, the same result to fp64 rounding.
+   Applies to one-plane blocks only: blocks of several planes always keep KL / KU (far smaller than
+   their Dinv blocks), and the setup's memory check counts them */
 #define MAD_OPT_COARSE_NO_CHAIN 8u
 /* MAD_OPT_BENCHMARK_TRACE: mad_get_cycle_trace returns the reference's -DBENCHMARK history instead of
    one entry per cycle -- in VCYCLE / FMG, level 0's relative residual after every pre-smoothing

@@ -199,6 +199,9 @@ struct CoarseBlocks {
     return std::max(1, std::min(nplanes, target / q));
   }
 
+  // blocks of > 1 plane keep KL / KU whatever with_chain says: they are much smaller than Dinv_i
+  static bool keeps_chain(bool with_chain, int64_t mb, int64_t q) { return with_chain || mb > q; }
+
   // bytes this solver would hold on the device for a grid (before building it)
   static size_t estimate_bytes(int dim, const int64_t nn[3], int target, bool with_chain) {
     int64_t len[3] = {nn[0], nn[1], dim == 3 ? nn[2] : 1};
@@ -208,8 +211,9 @@ struct CoarseBlocks {
     const int64_t P = planes_per_block((int)q, (int)no, target);
     const int64_t mb = P * q, nb = (no + P - 1) / P;
     const int64_t last = N - (nb - 1) * mb;
-    // Dinv blocks + 3 q^2 of setup workspace (+ 2 nb q^2 of chain matrices)
-    const int64_t chain = with_chain ? 2 * nb : 0;
+    // Dinv blocks + 3 q^2 of setup workspace (+ 2 nb q^2 of chain matrices: with_chain, or blocks of
+    // > 1 plane, which build() always gives them -- the same predicate)
+    const int64_t chain = keeps_chain(with_chain, mb, q) ? 2 * nb : 0;
     return (size_t)(((nb - 1) * mb * mb + last * last) * 8 + (chain + 3) * q * q * 8 + N * 160);
   }
   // The chain's KL_i / KU_i (q x q each, formed at setup) make every chain step one GEMV launch.
@@ -320,7 +324,7 @@ struct CoarseBlocks {
     dmalloc((void**)&eval, sizeof(double) * ne);
     dmalloc((void**)&fcol, sizeof(int) * ne);
     dmalloc((void**)&fval, sizeof(double) * ne);
-    if (with_chain || mb > q) {  // blocks of > 1 plane: KL / KU are much smaller than Dinv_i
+    if (keeps_chain(with_chain, mb, q)) {  // blocks of > 1 plane: KL / KU are much smaller than Dinv_i
       dmalloc((void**)&kl, sizeof(double) * nb * q * q);
       dmalloc((void**)&ku, sizeof(double) * nb * q * q);
     }

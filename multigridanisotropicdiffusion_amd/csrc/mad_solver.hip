@@ -562,9 +562,10 @@ class Solver final : public SolverBase {
       L.peer = true;
     }
   }
-  // every mailbox filled through the mapped windows with the sending rank's pattern by the
-  // sweep's store / completion / counter pattern, every element checked on the receiving rank
-  // (collective; peer_ping_k / peer_pong_k)
+  // every mailbox of the window -- x buffers 0 and 1, the b mailboxes (buffer 2) -- filled through
+  // the mapped windows by the sweep's store / completion / counter pattern with a pattern of the
+  // sending rank and the buffer, every element checked on the receiving rank, every counter pair
+  // exercised and reset (collective; peer_ping_k / peer_pong_k)
   bool peer_selftest(LevelData<T>& L) {
     const int r = c_->comm.rank();
     const bool self = c_->comm.stand_in();
@@ -574,21 +575,26 @@ class Solver final : public SolverBase {
     uint32_t* ctl = peer_ctl(L.win, L);
     const uint32_t one = 1u;
     HIP_CHECK(hipMemcpyAsync(ctl + 6, &one, sizeof one, hipMemcpyHostToDevice, c_->stream));
-    // every rank's ok word is set before any neighbour's ping can count in
-    c_->comm.local_barrier(c_->stream);
-    hipLaunchKernelGGL((peer_ping_k<T>), dim3(nblk, 2), dim3(256), 0, c_->stream, peer_out(L, 0), n, top, r);
-    HIP_CHECK(hipGetLastError());
-    // the in-process transport's ranks share one device's hardware queues: all pings done first
-    c_->comm.local_barrier(c_->stream);
-    const T* mlo = L.g.zlo_ghost ? mailbox(L.win, L, 0, 0) : nullptr;
-    const T* mhi = L.g.zhi_ghost ? mailbox(L.win, L, 0, 1) : nullptr;
     const uint64_t tmo = peer_timeout_ticks_ / 10;  // 2 s
-    hipLaunchKernelGGL((peer_pong_k<T>), dim3(nblk, 2), dim3(256), 0, c_->stream, mlo, mhi, ctl + 0, ctl + 1,
-                       self ? r : r - 1, self ? r : r + 1, n, nblk, ctl + 6, tmo);
-    HIP_CHECK(hipGetLastError());
+    for (int buf = 0; buf < 3; ++buf) {
+      const int salt = 1024 * buf;  // peer_pattern stays < 2^24 (exact in fp32)
+      const int cb = buf == 2 ? 8 : 2 * buf;
+      // every rank's ok word is set (and the previous buffer's pongs done) before any ping counts in
+      c_->comm.local_barrier(c_->stream);
+      hipLaunchKernelGGL((peer_ping_k<T>), dim3(nblk, 2), dim3(256), 0, c_->stream, peer_out(L, buf), n, top,
+                         r + salt);
+      HIP_CHECK(hipGetLastError());
+      // the in-process transport's ranks share one device's hardware queues: all pings done first
+      c_->comm.local_barrier(c_->stream);
+      const T* mlo = L.g.zlo_ghost ? mailbox(L.win, L, buf, 0) : nullptr;
+      const T* mhi = L.g.zhi_ghost ? mailbox(L.win, L, buf, 1) : nullptr;
+      hipLaunchKernelGGL((peer_pong_k<T>), dim3(nblk, 2), dim3(256), 0, c_->stream, mlo, mhi, ctl + cb,
+                         ctl + cb + 1, (self ? r : r - 1) + salt, (self ? r : r + 1) + salt, n, nblk, ctl + 6, tmo);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemsetAsync(ctl + cb, 0, 2 * sizeof(uint32_t), c_->stream));  // this buffer's counters
+    }
     uint32_t ok = 0;
     HIP_CHECK(hipMemcpyAsync(&ok, ctl + 6, sizeof ok, hipMemcpyDeviceToHost, c_->stream));
-    HIP_CHECK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), c_->stream));  // counters of buffer 0
     HIP_CHECK(hipStreamSynchronize(c_->stream));
     return c_->comm.all_true(ok == 1u, c_->stream);
   }
