@@ -16,8 +16,10 @@
 
 #include <array>
 #include <cstdint>
+#include <fstream>
 #include <iostream>
 #include <memory>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -151,6 +153,14 @@ class MultigridAnisotropicDiffusionImageFilter {
   // MI355X execution options (no reference counterpart)
   void SetPrecision(int32_t p) { desc_.precision = p; desc_.stall_guard = (p != MAD_FP64); }
   void SetDevice(int32_t d) { desc_.device = d; }
+  // the reference's -DBENCHMARK build (.hxx:145-151, 222-227, 401-409, 450-458, 477-485): Update()
+  // records the relres / seconds history (MAD_OPT_BENCHMARK_TRACE) and writes it to benchmark.txt as
+  // "relres_seconds" lines.  On by default when this header is compiled with -DBENCHMARK, as there.
+  void SetBenchmark(bool on) {
+    desc_.options = on ? (desc_.options | MAD_OPT_BENCHMARK_TRACE) : (desc_.options & ~MAD_OPT_BENCHMARK_TRACE);
+  }
+  // the history of the last Update() with SetBenchmark(true), one "relres_seconds" line per entry
+  std::vector<std::string> GetBenchmarkOutput() const { return bench_; }
 
   // SetDiffusionTensor (.hxx:66-101): copied and cast to fp64 at call time
   void SetDiffusionTensor(const InputTensorImageType* t) {
@@ -187,15 +197,35 @@ class MultigridAnisotropicDiffusionImageFilter {
     const int rc = mad_run(ctx_, input_->GetBufferPointer(), itkshim::PixelTraits<InputPixelType>::id,
                            output_->GetBufferPointer(), itkshim::PixelTraits<OutputPixelType>::id, &stats_);
     converged_ = check_run(rc, "mad", mad_last_error(ctx_));
+    bench_.clear();
+    if (d.options & MAD_OPT_BENCHMARK_TRACE) {
+      uint32_t n = 0;
+      check(mad_get_cycle_trace(ctx_, 0, nullptr, nullptr, nullptr, &n), ctx_);
+      std::vector<double> rr(n), sec(n);
+      check(mad_get_cycle_trace(ctx_, n, nullptr, rr.data(), sec.data(), &n), ctx_);
+      std::ofstream f("benchmark.txt");  // m_BenchmarkOutput.open("benchmark.txt"), .hxx:147
+      for (uint32_t q = 0; q < n; ++q) {
+        std::ostringstream ln;
+        ln << rr[q] << "_" << (float)sec[q];  // .hxx:225: relres << "_" << (float) seconds
+        bench_.push_back(ln.str());
+        f << bench_.back() << std::endl;
+      }
+    }
   }
   // false when the stall guard ended a time step above the tolerance (MAD_ERR_NOT_CONVERGED)
   bool GetConverged() const { return converged_; }
 
  protected:
-  MultigridAnisotropicDiffusionImageFilter() { check(mad_desc_init(&desc_)); }
+  MultigridAnisotropicDiffusionImageFilter() {
+    check(mad_desc_init(&desc_));
+#ifdef BENCHMARK
+    SetBenchmark(true);
+#endif
+  }
 
  private:
   mad_desc desc_{};
+  std::vector<std::string> bench_;
   mad_ctx* ctx_ = nullptr;
   mad_stats stats_{};
   bool converged_ = true;

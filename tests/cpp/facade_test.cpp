@@ -2,11 +2,15 @@
 // test/itk2DDiffusionTest_WJ.cxx:47-109 uses the reference filter.
 //   facade_test host   -> host-only calls (no GPU): defaults + depth rule
 //   facade_test run    -> 2D filter run on the GPU, prints the output checksum
+//   facade_test run bench -> the same with SetBenchmark(true) (the reference's -DBENCHMARK build):
+//                         2 nu + 1 "relres_seconds" lines per V-cycle in ./benchmark.txt
 //   facade_test ved    -> VEDMultigridImageFilter on a short 3D volume with a bright tube,
 //                         set up like test/itkVEDTest_GS.cxx:46-95
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
+#include <string>
 
 #include "mad_itk.hpp"
 
@@ -56,6 +60,7 @@ static int run_ved() {
 int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "ved") == 0) return run_ved();
   const bool run = argc > 1 && std::strcmp(argv[1], "run") == 0;
+  const bool bench = run && argc > 2 && std::strcmp(argv[2], "bench") == 0;
   mad_desc d;
   mad_desc_init(&d);
   if (d.iterations_per_grid != 2 || d.max_cycles != 100 || d.time_step != 0.01) return 2;
@@ -89,7 +94,18 @@ int main(int argc, char** argv) {
   filter->SetMaxCycles(100);
   filter->SetTolerance(1e-6);
   filter->SetCycle(FilterType::VCYCLE);
+  if (bench) filter->SetBenchmark(true);
   filter->Update();
+  if (bench) {
+    const auto lines = filter->GetBenchmarkOutput();
+    std::ifstream f("benchmark.txt");
+    std::string ln;
+    size_t nf = 0;
+    while (std::getline(f, ln)) nf += ln.find('_') != std::string::npos;
+    std::printf("benchmark lines=%zu file=%zu first=%s last=%s\n", lines.size(), nf,
+                lines.empty() ? "" : lines.front().c_str(), lines.empty() ? "" : lines.back().c_str());
+    if (lines.size() != 5u * filter->GetStats().total_cycles || nf != lines.size()) return 6;
+  }
   double sum = 0.0;
   auto out = filter->GetOutput();
   for (int64_t i = 0; i < out->NumberOfPixels(); ++i) sum += out->GetBufferPointer()[i];

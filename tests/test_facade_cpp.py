@@ -34,6 +34,18 @@ def test_facade_runs_filter(exe):
 
 
 @pytest.mark.gpu
+def test_facade_benchmark_output(exe, tmp_path):
+    """SetBenchmark(true), the reference's -DBENCHMARK build: benchmark.txt in the working
+    directory with 2 nu + 1 "relres_seconds" lines per V-cycle (MAD.hxx:401-409, 450-458, 477-485)."""
+    r = subprocess.run([exe, "run", "bench"], capture_output=True, text=True, timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "run ok" in r.stdout and "benchmark lines=" in r.stdout
+    lines = (tmp_path / "benchmark.txt").read_text().split()
+    rel = [float(ln.split("_")[0]) for ln in lines]
+    assert len(lines) % 5 == 0 and rel[-1] <= 1e-6
+
+
+@pytest.mark.gpu
 def test_facade_runs_ved_filter(exe):
     r = subprocess.run([exe, "ved"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
