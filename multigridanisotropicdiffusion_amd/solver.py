@@ -305,6 +305,16 @@ class Solver:
         self._check(self._L.mad_get_cycle_trace(self._ctx, k, st, rr, sec, ctypes.byref(n)))
         return [(st[q], rr[q], sec[q]) for q in range(k)]
 
+    def placement_trials(self):
+        """Level-0 sweep ms on each set of level-0 arrays the last setup tried (mad_placement_trials;
+        the fastest was kept); [] when nothing was tuned."""
+        n = ctypes.c_uint32()
+        self._check(self._L.mad_placement_trials(self._ctx, 0, None, ctypes.byref(n)))
+        k = n.value
+        ms = (ctypes.c_double * max(k, 1))()
+        self._check(self._L.mad_placement_trials(self._ctx, k, ms, ctypes.byref(n)))
+        return [ms[q] for q in range(k)]
+
     @property
     def resolved_precision(self):
         """The precision mad_create resolved (PRECISION_AUTO -> FP32 or FP32_REFINE)."""

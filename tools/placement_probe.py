@@ -18,7 +18,9 @@ sys.path.insert(0, ROOT)
 
 
 def sweep_ms(M):
-    s = M.Solver((512, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=M.SMOOTHER)
+    opt = M.capi.OPT_NO_PLACEMENT_TUNE if os.environ.get("MAD_PROBE_NOTUNE") == "1" else 0
+    s = M.Solver((512, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=M.SMOOTHER,
+                 options=opt)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
@@ -35,8 +37,8 @@ def one(spacer_mib):
         assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(spacer_mib << 20)) == 0
     import multigridanisotropicdiffusion_amd as M
     s, kern = sweep_ms(M)
-    print(json.dumps({"spacer_mib": spacer_mib, "spacer_ptr": hex(p.value or 0), "kernel_ms": round(kern, 4)}),
-          flush=True)
+    print(json.dumps({"spacer_mib": spacer_mib, "spacer_ptr": hex(p.value or 0), "kernel_ms": round(kern, 4),
+                      "placement_trials": [round(v, 4) for v in s.placement_trials()]}), flush=True)
 
 
 def order(n, free=False, prealloc=0):
@@ -65,14 +67,20 @@ def places(specs, reps):
         for spec in specs:
             env = dict(os.environ)
             env.pop("MAD_LEVEL0_PLACE", None)
-            if spec != "sep":
+            env["MAD_LEVEL0_REPORT"] = "1"
+            env.pop("MAD_PROBE_NOTUNE", None)
+            if spec == "notune":  # the first allocation, as before round 6
+                env["MAD_PROBE_NOTUNE"] = "1"
+            elif spec not in ("sep", "tune"):
                 env["MAD_LEVEL0_PLACE"] = spec
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", "0"], capture_output=True,
                                text=True, timeout=120, env=env)
             out = r.stdout.strip()
-            kern = json.loads(out)["kernel_ms"] if r.returncode == 0 and out else None
+            res = json.loads(out) if r.returncode == 0 and out else {}
+            kern = res.get("kernel_ms")
             notes = [ln for ln in r.stderr.splitlines() if ln.startswith("[mad]")]
-            print(json.dumps({"rep": rep, "place": spec, "kernel_ms": kern, "notes": notes}) if kern else
+            print(json.dumps({"rep": rep, "place": spec, "kernel_ms": kern, "trials": res.get("placement_trials"),
+                              "notes": notes}) if kern else
                   f"{spec}: rc {r.returncode} {r.stderr[-400:]}", flush=True)
             if r.returncode != 0:
                 return 1
