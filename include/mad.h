@@ -197,7 +197,7 @@ typedef struct mad_desc {
    correction cycles' entries are the fp32 residual of the correction equation over the step's
    ||b||, i.e. the relres of the updated iterate to fp32 rounding. */
 #define MAD_OPT_BENCHMARK_TRACE 16u
-/* MAD_OPT_NO_PLACEMENT_TUNE: keep level 0's first allocation (mad_placement_trials; the A/B of the tuning) */
+/* MAD_OPT_NO_PLACEMENT_TUNE: keep level 0's first ping-pong allocation (mad_placement_trials; the A/B) */
 #define MAD_OPT_NO_PLACEMENT_TUNE 32u
 
 typedef struct mad_stats {
@@ -266,12 +266,12 @@ int mad_get_step_stats(const mad_ctx *ctx, uint32_t step, uint32_t *cycles, doub
  * records.  Copies min(cap, total) entries (any pointer may be NULL); *count = total entries. */
 int mad_get_cycle_trace(const mad_ctx *ctx, uint32_t cap, uint32_t *step, double *relres,
                         double *seconds, uint32_t *count);
-/* Level-0 placement tuning of the last setup (no reference counterpart): the level-0 sweep's time in ms
- * on each set of the level's arrays setup tried, in order (the first is the initial allocation; the
- * fastest was kept).  The sweep's speed depends on where its ~7 GB of arrays land in HBM (1.13 / 1.18 /
- * 1.25 ms at 512^3 from one allocation to the next, profiles/r06_placement.md), so setup times up to
- * four allocations of single-rank 3D levels of >= 2^24 voxels and keeps the fastest.  *count = 0 when
- * nothing was tuned (smaller levels, rank slabs, MAD_OPT_NO_PLACEMENT_TUNE). */
+/* Level-0 placement tuning of the last setup (no reference counterpart).  The level-0 sweep's speed
+ * depends on where its ping-pong pair (x, t) landed in HBM: per allocation, each direction of the pair
+ * sweeps in ~1.13 or ~1.24 ms at 512^3 (profiles/r06_placement.md).  Setup times both directions and,
+ * while one is slower than the fastest direction seen, tries up to 7 fresh allocations of the pair,
+ * keeping the fastest.  ms receives (forward, reverse) sweep ms per pair tried, in order; *count =
+ * 2 x pairs, 0 when nothing was tuned (levels < 2^24 voxels, rank slabs, MAD_OPT_NO_PLACEMENT_TUNE). */
 int mad_placement_trials(const mad_ctx *ctx, uint32_t cap, double *ms, uint32_t *count);
 
 /* ---------------------------------------------------------------- hierarchy */

@@ -495,93 +495,128 @@ class Solver final : public SolverBase {
   }
 
   // ------------------------------------------------------------- level-0 placement
-  // The level-0 sweep streams ~7 GB per launch at 512^3, and how fast depends on where its arrays
-  // landed in physical memory: the same kernel on the same box sweeps in 1.13, 1.18 or 1.25 ms from
-  // one allocation of the level's arrays to the next, with the same HBM bytes, the same L2 hit rate
-  // and ~7 K UTCL1 misses per launch in every mode (profiles/r06_placement.md).  So setup times the
-  // level's own sweep on its arrays and on up to PLACEMENT_TRIES - 1 fresh allocations of them (the
-  // contents copied over: everything but the records is still zero here) and keeps the fastest set;
-  // the others are freed.  Single-rank 3D levels of >= 2^24 voxels whose sweep is the fused GS or WJ
-  // sweep, with the memory for a second set; MAD_OPT_NO_PLACEMENT_TUNE keeps the first allocation.
-  static constexpr int PLACEMENT_TRIES = 4;
+  // The level-0 sweep streams ~7 GB per launch at 512^3, and on some boxes its speed depends on where
+  // its arrays landed in physical memory: per allocation, each direction of the ping-pong pair (read x
+  // / write t, then read t / write x) sweeps in ~1.13 or in ~1.24 ms -- the same kernel, the same HBM
+  // bytes, the same L2 hit rate and ~7 K UTCL1 misses per launch in every case, the clocks steady; on
+  // other boxes every allocation runs 1.24 ms (profiles/r06_placement.md).  So setup times both
+  // directions of the level's own sweep on its arrays and on fresh allocations of them (the pair each
+  // time, the records too every second time; contents copied over) and keeps the fastest set, the
+  // others freed: until both directions of the kept set are within 2 % of the fastest direction seen
+  // once the two speeds have shown up, at most PLACEMENT_TRIES sets.  3D levels of >= 2^24 voxels
+  // (a rank's slab too: 512 x 512 x 64 on 8 ranks) whose sweep is the fused GS sweep -- timed as the
+  // plain whole-slab launch, no exchange, so every rank decides alone -- or, on one rank, the WJ sweep;
+  // with the memory for a second set.  Not on the in-process transport (its ranks share one device).
+  // MAD_OPT_NO_PLACEMENT_TUNE keeps the first allocation.
+  static constexpr int PLACEMENT_TRIES = 8;
   void tune_level0_placement() {
     tuned_ms_.clear();
-    if (lv_.empty() || c_->dim != 3 || c_->comm.active() || (c_->d.options & MAD_OPT_NO_PLACEMENT_TUNE)) return;
+    if (lv_.empty() || c_->dim != 3 || (c_->d.options & MAD_OPT_NO_PLACEMENT_TUNE)) return;
+    if (c_->comm.active() && c_->comm.mode() == Comm::LOCAL) return;
     LevelData<T>& L = lv_[0];
     const int sm = c_->d.smoother;
     if (L.pool || L.g.N < ((int64_t)1 << 24) || sm == MAD_GAUSS_SEIDEL_LEX) return;
-    if (sm == MAD_GAUSS_SEIDEL && !use_fused(0)) return;
+    const bool fused = sm == MAD_GAUSS_SEIDEL && use_fused(0);
+    if (!fused && (sm == MAD_GAUSS_SEIDEL || c_->comm.active())) return;
     const int64_t margin = margin_elems(L.g);
-    const int64_t tot = L.g.N + 2 * (L.ghost + margin);
+    const size_t pbytes = sizeof(T) * (size_t)(L.g.N + 2 * (L.ghost + margin));
     const int64_t cplane = L.g.sz * L.g.rs;
-    const int64_t ctot = (L.g.nz + 2 * GHOST) * cplane + 2 * margin * L.g.rs;
-    const size_t bytes[5] = {sizeof(T) * tot, sizeof(T) * tot, sizeof(T) * tot, sizeof(T) * tot,
-                             sizeof(T) * ctot};
-    size_t set = 0;
-    for (size_t v : bytes) set += v;
-    // the level's ping-pong pair is back in place after an even number of sweeps
-    auto time_set = [&]() {
-      double tot_ms = 0.0, kern = 0.0;
-      unsigned n = 0;
-      bench_smooth(0, 4, &tot_ms, &kern, &n);
-      std::vector<float> v(launch_ms.begin() + 1, launch_ms.end());  // the first launch is cold
-      std::sort(v.begin(), v.end());
-      return v.empty() ? kern : (double)v[v.size() / 2];
+    const size_t cbytes = sizeof(T) * (size_t)((L.g.nz + 2 * GHOST) * cplane + 2 * margin * L.g.rs);
+    struct Set {
+      T* x;
+      T* t;
+      T* cf;
     };
-    auto point = [&](T* const a[4], T* cfa) {
-      for (int q = 0; q < 4; ++q) L.alloc[q] = a[q];
-      L.cf_alloc = cfa;
-      L.x = L.alloc[0] + margin + L.ghost;
-      L.b = L.alloc[1] + margin + L.ghost;
-      L.r = L.alloc[2] + margin + L.ghost;
-      L.t = L.alloc[3] + margin + L.ghost;
-      L.cf = L.cf_alloc + margin * L.g.rs + GHOST * cplane;
+    auto point = [&](const Set& a) {  // after an even number of sweeps alloc[0] is x's, alloc[3] t's
+      L.alloc[0] = a.x;
+      L.alloc[3] = a.t;
+      L.cf_alloc = a.cf;
+      L.x = a.x + margin + L.ghost;
+      L.t = a.t + margin + L.ghost;
+      L.cf = a.cf + margin * L.g.rs + GHOST * cplane;
       L.phys[0] = L.x;
       L.phys[1] = L.t;
     };
-    double best = time_set();
-    tuned_ms_.push_back(best);
+    // mean ms of the two launches in each direction: 0 and 2 read x and write t, 1 and 3 the reverse
+    double fastest = INFINITY, slowest = 0.0;
+    // fused GS: the plain whole-slab launch on the level's arrays (rank slabs: no exchange; the ghost
+    // planes hold zeros like everything but the records here), swapping the pair like the sweep
+    auto sweeps = [&](unsigned n) {
+      if (!fused) {
+        double tot_ms = 0.0, kern = 0.0;
+        unsigned q = 0;
+        bench_smooth(0, n, &tot_ms, &kern, &q);
+        return;
+      }
+      std::vector<hipEvent_t> ev(2 * n);
+      for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+      for (unsigned i = 0; i < n; ++i) {
+        HIP_CHECK(hipEventRecord(ev[2 * i], c_->stream));
+        launch_fused_part(L, 0);
+        HIP_CHECK(hipEventRecord(ev[2 * i + 1], c_->stream));
+        std::swap(L.x, L.t);
+        std::swap(L.alloc[0], L.alloc[3]);
+      }
+      HIP_CHECK(hipEventSynchronize(ev[2 * n - 1]));
+      launch_ms.assign(n, 0.f);
+      for (unsigned i = 0; i < n; ++i) HIP_CHECK(hipEventElapsedTime(&launch_ms[i], ev[2 * i], ev[2 * i + 1]));
+      for (auto& e : ev) (void)hipEventDestroy(e);
+    };
+    auto time_dirs = [&](double* fwd, double* rev) {
+      sweeps(4);
+      *fwd = 0.5 * (launch_ms[0] + launch_ms[2]);
+      *rev = 0.5 * (launch_ms[1] + launch_ms[3]);
+      tuned_ms_.push_back(*fwd);
+      tuned_ms_.push_back(*rev);
+      fastest = std::min({fastest, *fwd, *rev});
+      slowest = std::max({slowest, *fwd, *rev});
+    };
+    sweeps(16);  // the clocks ramp up over the first ~20 launches after the device idled (r06_clock_summaries)
+    Set best{L.alloc[0], L.alloc[3], L.cf_alloc};
+    double bf = 0.0, br = 0.0;
+    time_dirs(&bf, &br);
     for (int tr = 1; tr < PLACEMENT_TRIES; ++tr) {
+      // the kept set is at the fast speed, and a slower one has been seen (so that speed is the fast one)
+      if (slowest > 1.05 * fastest && std::max(bf, br) <= 1.02 * fastest) break;
+      const bool with_cf = (tr % 2) == 0;
       size_t free_b = 0, total_b = 0;
       HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-      if (free_b < set + set / 4) break;
-      T* cur[4] = {L.alloc[0], L.alloc[1], L.alloc[2], L.alloc[3]};
-      T* cur_cf = L.cf_alloc;
-      T* cand[4] = {nullptr, nullptr, nullptr, nullptr};
-      T* cand_cf = nullptr;
-      bool ok = true;
-      for (int q = 0; q < 4 && ok; ++q) ok = contiguous_alloc((void**)&cand[q], bytes[q]) == hipSuccess;
-      if (ok) ok = contiguous_alloc((void**)&cand_cf, bytes[4]) == hipSuccess;
+      if (free_b < 2 * (2 * pbytes + (with_cf ? cbytes : 0)) + ((size_t)1 << 30)) break;
+      Set cand{nullptr, nullptr, with_cf ? nullptr : best.cf};
+      bool ok = contiguous_alloc((void**)&cand.x, pbytes) == hipSuccess &&
+                contiguous_alloc((void**)&cand.t, pbytes) == hipSuccess &&
+                (!with_cf || contiguous_alloc((void**)&cand.cf, cbytes) == hipSuccess);
       if (!ok) {
         (void)hipGetLastError();
-        for (T* a : cand)
-          if (a) (void)hipFree(a);
-        if (cand_cf) (void)hipFree(cand_cf);
+        if (cand.x) (void)hipFree(cand.x);
+        if (cand.t) (void)hipFree(cand.t);
+        if (with_cf && cand.cf) (void)hipFree(cand.cf);
         break;
       }
-      for (int q = 0; q < 4; ++q)
-        HIP_CHECK(hipMemcpyAsync(cand[q], cur[q], bytes[q], hipMemcpyDeviceToDevice, c_->stream));
-      HIP_CHECK(hipMemcpyAsync(cand_cf, cur_cf, bytes[4], hipMemcpyDeviceToDevice, c_->stream));
-      point(cand, cand_cf);
-      const double ms = time_set();
-      tuned_ms_.push_back(ms);
-      T* const* loser = cand;
-      T* loser_cf = cand_cf;
-      if (ms < best) {  // keep the candidate
-        best = ms;
-        loser = cur;
-        loser_cf = cur_cf;
+      HIP_CHECK(hipMemcpyAsync(cand.x, best.x, pbytes, hipMemcpyDeviceToDevice, c_->stream));
+      HIP_CHECK(hipMemcpyAsync(cand.t, best.t, pbytes, hipMemcpyDeviceToDevice, c_->stream));
+      if (with_cf) HIP_CHECK(hipMemcpyAsync(cand.cf, best.cf, cbytes, hipMemcpyDeviceToDevice, c_->stream));
+      point(cand);
+      double f = 0.0, r = 0.0;
+      time_dirs(&f, &r);
+      Set loser = cand;
+      if (f + r < bf + br) {  // keep the candidate
+        loser = best;
+        best = cand;
+        bf = f;
+        br = r;
       } else {
-        point(cur, cur_cf);
+        point(best);
       }
       HIP_CHECK(hipStreamSynchronize(c_->stream));
-      for (int q = 0; q < 4; ++q) HIP_CHECK(hipFree(loser[q]));
-      HIP_CHECK(hipFree(loser_cf));
+      HIP_CHECK(hipFree(loser.x));
+      HIP_CHECK(hipFree(loser.t));
+      if (loser.cf != best.cf) HIP_CHECK(hipFree(loser.cf));
     }
     x_changed(0);
     L.b_halo_ok = L.brec_ok = false;
   }
-  std::vector<double> tuned_ms_;  // per-candidate level-0 sweep ms of the last placement tuning
+  std::vector<double> tuned_ms_;  // per candidate pair: forward, reverse level-0 sweep ms (last setup)
   std::vector<double> placement_ms() const override { return tuned_ms_; }
 
   // level arrays (x, b, r, t, coefficient records): mad_alloc.hpp

@@ -80,13 +80,24 @@ def main():
             f.write(json.dumps(r) + "\n")
     mets = [json.loads(ln) for ln in open(os.path.join(out, "metrics.jsonl"))]
     full = [m for m in mets if "full" in m]
-    if full:
+    if full and os.environ.get("CLOCK_PROBE_TIMELINE") == "1":
         print("metrics fields:", json.dumps(full[0]["full"])[:3000])
     mets = [m for m in mets if "m" in m]
     keys = [k for k in ("current_gfxclk", "current_gfxclks", "current_uclk", "current_socclk", "current_socclks",
                         "current_fclk", "average_socket_power", "current_socket_power", "temperature_hotspot",
                         "temperature_mem", "throttle_status", "indep_throttle_status")
             if any(k in m["m"] for m in mets)]
+    allk = sorted(v for r in rows for v in r["ms"])
+    summ = {"launches": len(allk), "kern_mean": round(sum(allk) / len(allk), 4),
+            "kern_median": allk[len(allk) // 2], "frac_over_1.2ms": round(sum(v > 1.2 for v in allk) / len(allk), 3)}
+    for k in keys:
+        vals = [m["m"][k] for m in mets if k in m["m"]]
+        if vals:
+            summ[k] = round(sum(vals) / len(vals), 1)
+    print("SUMMARY " + json.dumps(summ), flush=True)
+    if os.environ.get("CLOCK_PROBE_TIMELINE") != "1":
+        s.close()
+        return
     print("window_start  n  kern_mean kern_min kern_max | " + " ".join(keys))
     t = rows[0]["t0"] if rows else time.time()
     while rows and t < rows[-1]["t1"]:

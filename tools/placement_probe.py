@@ -19,7 +19,8 @@ sys.path.insert(0, ROOT)
 
 def sweep_ms(M):
     opt = M.capi.OPT_NO_PLACEMENT_TUNE if os.environ.get("MAD_PROBE_NOTUNE") == "1" else 0
-    s = M.Solver((512, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=M.SMOOTHER,
+    cyc = M.VCYCLE if os.environ.get("MAD_PROBE_LAYOUT") == "vcycle" else M.SMOOTHER
+    s = M.Solver((512, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=cyc,
                  options=opt)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
@@ -64,11 +65,16 @@ def places(specs, reps):
     (MAD_LEVEL0_PLACE, csrc/mad_alloc.hpp Placement; "sep" = separate allocations), fresh process
     each, the specs alternated `reps` times"""
     for rep in range(reps):
-        for spec in specs:
+        for label in specs:
+            spec = label
             env = dict(os.environ)
             env.pop("MAD_LEVEL0_PLACE", None)
             env["MAD_LEVEL0_REPORT"] = "1"
             env.pop("MAD_PROBE_NOTUNE", None)
+            env.pop("MAD_PROBE_LAYOUT", None)
+            if spec.startswith("vcycle"):  # the V-cycle layout's level-0 sweep (36-B records, dense b)
+                env["MAD_PROBE_LAYOUT"] = "vcycle"
+                spec = spec[len("vcycle"):].lstrip("-") or "tune"
             if spec == "notune":  # the first allocation, as before round 6
                 env["MAD_PROBE_NOTUNE"] = "1"
             elif spec not in ("sep", "tune"):
@@ -79,9 +85,9 @@ def places(specs, reps):
             res = json.loads(out) if r.returncode == 0 and out else {}
             kern = res.get("kernel_ms")
             notes = [ln for ln in r.stderr.splitlines() if ln.startswith("[mad]")]
-            print(json.dumps({"rep": rep, "place": spec, "kernel_ms": kern, "trials": res.get("placement_trials"),
+            print(json.dumps({"rep": rep, "place": label, "kernel_ms": kern, "trials": res.get("placement_trials"),
                               "notes": notes}) if kern else
-                  f"{spec}: rc {r.returncode} {r.stderr[-400:]}", flush=True)
+                  f"{label}: rc {r.returncode} {r.stderr[-400:]}", flush=True)
             if r.returncode != 0:
                 return 1
     return 0
