@@ -292,8 +292,6 @@ struct LevelData {
   T* t = nullptr;  // WJ ping-pong / scratch
   T* cf = nullptr;        // field 0, plane 0 (ghost planes precede it on rank slabs)
   T* cf_alloc = nullptr;
-  char* pool = nullptr;   // the one allocation alloc[] / cf_alloc are carved from (mad_alloc.hpp Placement)
-  void* pool_own[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // arrays placed outside it
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -378,7 +376,6 @@ class Solver final : public SolverBase {
       // up to a tile halo outside the outermost (ghost) plane
       const int64_t margin = margin_elems(L.g);
       const int64_t tot = L.g.N + 2 * (L.ghost + margin);
-      // (record stride first: a pooled level 0 sizes its record array with it)
       bool brec_on = c->d.cycle == MAD_SMOOTHER;
       if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
       L.brec = (dim == 3 && l == 0 && brec_on);
@@ -387,32 +384,12 @@ class Solver final : public SolverBase {
       const int64_t cgp = (dim == 3) ? GHOST : 0;
       const int64_t cmargin = margin * L.g.rs;
       const int64_t ctot = (L.g.nz + 2 * cgp) * cplane + 2 * cmargin;
-      const Placement place = (l == 0 && dim == 3) ? level0_placement() : Placement{};
-      if (place.on) {
-        const size_t bytes[5] = {sizeof(T) * tot, sizeof(T) * tot, sizeof(T) * tot, sizeof(T) * tot,
-                                 sizeof(T) * ctot};
-        size_t at[5];
-        const size_t pool = place_offsets(place, bytes, at);
-        HIP_CHECK(contiguous_alloc((void**)&L.pool, pool));
-        HIP_CHECK(hipMemsetAsync(L.pool, 0, pool, c->stream));
-        T** dst[5] = {&L.alloc[0], &L.alloc[1], &L.alloc[2], &L.alloc[3], &L.cf_alloc};
-        for (int a = 0; a < 5; ++a) {
-          if (place.own[a]) {
-            level_alloc((void**)dst[a], bytes[a]);
-            HIP_CHECK(hipMemsetAsync(*dst[a], 0, bytes[a], c->stream));
-            L.pool_own[a] = *dst[a];
-          } else {
-            *dst[a] = (T*)(L.pool + at[a]);
-          }
-        }
-      } else {
-        for (int a = 0; a < 4; ++a) {
-          level_alloc((void**)&L.alloc[a], sizeof(T) * tot);
-          HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
-        }
-        level_alloc((void**)&L.cf_alloc, sizeof(T) * ctot);
-        HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
+      for (int a = 0; a < 4; ++a) {
+        level_alloc((void**)&L.alloc[a], sizeof(T) * tot);
+        HIP_CHECK(hipMemsetAsync(L.alloc[a], 0, sizeof(T) * tot, c->stream));
       }
+      level_alloc((void**)&L.cf_alloc, sizeof(T) * ctot);
+      HIP_CHECK(hipMemsetAsync(L.cf_alloc, 0, sizeof(T) * ctot, c->stream));
       L.x = L.alloc[0] + margin + L.ghost;
       L.b = L.alloc[1] + margin + L.ghost;
       L.r = L.alloc[2] + margin + L.ghost;
@@ -430,9 +407,6 @@ class Solver final : public SolverBase {
       // it saves (VED diffusion 126 -> 116.5 ms without it, profiles/r01_brec_ab.log).
       // (L.brec / L.g.rs are set above, before the allocation)
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
-      if (l == 0 && std::getenv("MAD_LEVEL0_REPORT"))  // probe: where level 0's arrays landed (VAs)
-        std::fprintf(stderr, "[mad] level0 x %p b %p r %p t %p cf %p (pool %p)\n", (void*)L.alloc[0],
-                     (void*)L.alloc[1], (void*)L.alloc[2], (void*)L.alloc[3], (void*)L.cf_alloc, (void*)L.pool);
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
@@ -515,7 +489,7 @@ class Solver final : public SolverBase {
     if (c_->comm.active() && c_->comm.mode() == Comm::LOCAL) return;
     LevelData<T>& L = lv_[0];
     const int sm = c_->d.smoother;
-    if (L.pool || L.g.N < ((int64_t)1 << 24) || sm == MAD_GAUSS_SEIDEL_LEX) return;
+    if (L.g.N < ((int64_t)1 << 24) || sm == MAD_GAUSS_SEIDEL_LEX) return;
     const bool fused = sm == MAD_GAUSS_SEIDEL && use_fused(0);
     if (!fused && (sm == MAD_GAUSS_SEIDEL || c_->comm.active())) return;
     const int64_t margin = margin_elems(L.g);
@@ -2519,15 +2493,9 @@ class Solver final : public SolverBase {
       Comm::close_window(L.win_lo, L.win_ipc);
       Comm::close_window(L.win_hi, L.win_ipc);
       if (L.win) (void)hipFree(L.win);
-      if (L.pool) {
-        (void)hipFree(L.pool);
-        for (auto& a : L.pool_own)
-          if (a) (void)hipFree(a);
-      } else {
-        for (auto& a : L.alloc)
-          if (a) (void)hipFree(a);
-        if (L.cf_alloc) (void)hipFree(L.cf_alloc);
-      }
+      for (auto& a : L.alloc)
+        if (a) (void)hipFree(a);
+      if (L.cf_alloc) (void)hipFree(L.cf_alloc);
     }
     lv_.clear();
     for (auto& a : r64alloc_)

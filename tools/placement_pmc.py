@@ -3,7 +3,7 @@
 tools/placement_probe.py --one under `rocprofv3 --pmc GROUP` (one counter group per run, each run under its
 own time limit), and print per process the probe's kernel mean and the mean of every counter over the
 level-0 gs_fused3_k dispatches.
-    python tools/placement_pmc.py OUTDIR REPS "CTR CTR ..." ["CTR ..." ...]   (MAD_LEVEL0_PLACE passes through)"""
+    python tools/placement_pmc.py OUTDIR REPS "CTR CTR ..." ["CTR ..." ...]   (fresh processes, default setup)"""
 import csv
 import glob
 import json

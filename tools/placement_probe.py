@@ -6,7 +6,12 @@ build the bench's SMOOTHER-layout 512^3 solver and time its level-0 sweep (mean 
 40 launches after 5 warm-up sweeps); `--order N` builds N solvers one after another in the
 same process (all kept alive) and times each.
     python tools/placement_probe.py [spacer_mib ...]
-    python tools/placement_probe.py --order 3"""
+    python tools/placement_probe.py --order 3
+Round 6: `--places REPS SPEC ...` alternates fresh processes of the specs: tune (the default setup, with
+the level-0 placement tuning), notune (MAD_OPT_NO_PLACEMENT_TUNE), prefixed vcycle- (the V-cycle layout's
+sweep) or flip- (gs_kernel 4); each line carries the setup's placement trials (mad_placement_trials).
+The round-6 runs that carved the level's arrays from one block (MAD_LEVEL0_PLACE, profiles/r06_place*.log)
+used a probe hook of commit 21c67c3, removed since."""
 import ctypes
 import json
 import os
@@ -20,8 +25,9 @@ sys.path.insert(0, ROOT)
 def sweep_ms(M):
     opt = M.capi.OPT_NO_PLACEMENT_TUNE if os.environ.get("MAD_PROBE_NOTUNE") == "1" else 0
     cyc = M.VCYCLE if os.environ.get("MAD_PROBE_LAYOUT") == "vcycle" else M.SMOOTHER
+    # MAD_PROBE_GSK=4: the last z-chunk marched downward (mad_desc.gs_kernel 4)
     s = M.Solver((512, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=cyc,
-                 options=opt)
+                 options=opt, gs_kernel=int(os.environ.get("MAD_PROBE_GSK", "0")))
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
@@ -61,24 +67,24 @@ def order(n, free=False, prealloc=0):
 
 
 def places(specs, reps):
-    """round 6: level 0's arrays carved from one contiguous block at the given relative offsets
-    (MAD_LEVEL0_PLACE, csrc/mad_alloc.hpp Placement; "sep" = separate allocations), fresh process
-    each, the specs alternated `reps` times"""
+    """round 6: fresh process per spec, the specs alternated `reps` times (see the module doc)"""
     for rep in range(reps):
         for label in specs:
             spec = label
             env = dict(os.environ)
-            env.pop("MAD_LEVEL0_PLACE", None)
-            env["MAD_LEVEL0_REPORT"] = "1"
             env.pop("MAD_PROBE_NOTUNE", None)
             env.pop("MAD_PROBE_LAYOUT", None)
+            env.pop("MAD_PROBE_GSK", None)
+            if spec.startswith("flip"):  # gs_kernel 4: the second z-chunk marches downward
+                env["MAD_PROBE_GSK"] = "4"
+                spec = spec[len("flip"):].lstrip("-") or "tune"
             if spec.startswith("vcycle"):  # the V-cycle layout's level-0 sweep (36-B records, dense b)
                 env["MAD_PROBE_LAYOUT"] = "vcycle"
                 spec = spec[len("vcycle"):].lstrip("-") or "tune"
             if spec == "notune":  # the first allocation, as before round 6
                 env["MAD_PROBE_NOTUNE"] = "1"
             elif spec not in ("sep", "tune"):
-                env["MAD_LEVEL0_PLACE"] = spec
+                raise SystemExit(f"unknown spec {label}")
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", "0"], capture_output=True,
                                text=True, timeout=120, env=env)
             out = r.stdout.strip()
