@@ -267,7 +267,7 @@ struct SolverBase {
   virtual void bench_vcycle(unsigned n, double* total_ms) = 0;
   virtual void synth_level(int l, int which, uint64_t seed) = 0;
   virtual std::string smooth_kernel(int l) = 0;
-  // level-0 sweep ms of every placement candidate setup timed (Solver::tune_level0_placement)
+  // level-0 sweep ms of every placement candidate setup timed (Solver::tune_placement)
   virtual std::vector<double> placement_ms() const { return {}; }
 };
 
@@ -464,7 +464,8 @@ class Solver final : public SolverBase {
     build_operators();
     build_coarse_inverse();
     setup_peer();
-    tune_level0_placement();
+    tuned_ms_.clear();
+    for (int l = 0; l < nl; ++l) tune_placement(l);  // levels of >= 2^24 voxels: 0, and 1 at 512^3
     HIP_CHECK(hipStreamSynchronize(c->stream));
   }
 
@@ -481,16 +482,16 @@ class Solver final : public SolverBase {
   // (a rank's slab too: 512 x 512 x 64 on 8 ranks) whose sweep is the fused GS sweep -- timed as the
   // plain whole-slab launch, no exchange, so every rank decides alone -- or, on one rank, the WJ sweep;
   // with the memory for a second set.  Not on the in-process transport (its ranks share one device).
-  // MAD_OPT_NO_PLACEMENT_TUNE keeps the first allocation.
+  // MAD_OPT_NO_PLACEMENT_TUNE keeps the first allocation.  Every level of >= 2^24 voxels is tuned so
+  // (level 1 of a 512^3 grid too); mad_placement_trials reports level 0's trials.
   static constexpr int PLACEMENT_TRIES = 8;
-  void tune_level0_placement() {
-    tuned_ms_.clear();
-    if (lv_.empty() || c_->dim != 3 || (c_->d.options & MAD_OPT_NO_PLACEMENT_TUNE)) return;
+  void tune_placement(int l) {
+    if (c_->dim != 3 || (c_->d.options & MAD_OPT_NO_PLACEMENT_TUNE)) return;
     if (c_->comm.active() && c_->comm.mode() == Comm::LOCAL) return;
-    LevelData<T>& L = lv_[0];
+    LevelData<T>& L = lv_[l];
     const int sm = c_->d.smoother;
     if (L.g.N < ((int64_t)1 << 24) || sm == MAD_GAUSS_SEIDEL_LEX) return;
-    const bool fused = sm == MAD_GAUSS_SEIDEL && use_fused(0);
+    const bool fused = sm == MAD_GAUSS_SEIDEL && use_fused(l);
     if (!fused && (sm == MAD_GAUSS_SEIDEL || c_->comm.active())) return;
     const int64_t margin = margin_elems(L.g);
     const size_t pbytes = sizeof(T) * (size_t)(L.g.N + 2 * (L.ghost + margin));
@@ -519,7 +520,7 @@ class Solver final : public SolverBase {
       if (!fused) {
         double tot_ms = 0.0, kern = 0.0;
         unsigned q = 0;
-        bench_smooth(0, n, &tot_ms, &kern, &q);
+        bench_smooth(l, n, &tot_ms, &kern, &q);
         return;
       }
       std::vector<hipEvent_t> ev(2 * n);
@@ -540,8 +541,10 @@ class Solver final : public SolverBase {
       sweeps(4);
       *fwd = 0.5 * (launch_ms[0] + launch_ms[2]);
       *rev = 0.5 * (launch_ms[1] + launch_ms[3]);
-      tuned_ms_.push_back(*fwd);
-      tuned_ms_.push_back(*rev);
+      if (l == 0) {
+        tuned_ms_.push_back(*fwd);
+        tuned_ms_.push_back(*rev);
+      }
       fastest = std::min({fastest, *fwd, *rev});
       slowest = std::max({slowest, *fwd, *rev});
     };
@@ -587,7 +590,7 @@ class Solver final : public SolverBase {
       HIP_CHECK(hipFree(loser.t));
       if (loser.cf != best.cf) HIP_CHECK(hipFree(loser.cf));
     }
-    x_changed(0);
+    x_changed(l);
     L.b_halo_ok = L.brec_ok = false;
   }
   std::vector<double> tuned_ms_;  // per candidate pair: forward, reverse level-0 sweep ms (last setup)

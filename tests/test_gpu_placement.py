@@ -1,4 +1,4 @@
-"""Level-0 placement tuning at setup (Solver::tune_level0_placement, mad_placement_trials).
+"""Level-0 placement tuning at setup (Solver::tune_placement, mad_placement_trials).
 
 The level-0 sweep's speed depends on where its arrays landed in HBM (profiles/r06_placement.md), so setup
 times both directions of the sweep on fresh allocations of the level's arrays and keeps the fastest set.
