@@ -21,6 +21,7 @@ SMOOTHER-mode solver of the sweep measurement.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -37,6 +38,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    # untimed sweeps after setup, before the W warm-up steps: the clocks and power take ~20-30 launches
+    # (~30 ms) to reach their steady state after the device idled (profiles/r06_clock_summaries.log)
+    p.add_argument("--settle-ms", type=float, default=150.0)
     p.add_argument("--size", type=int, default=512)
     # 20 graph replays (~0.16 s): a per-cycle figure above the ~0.3 ms box-to-box noise
     p.add_argument("--vcycles", type=int, default=20)
@@ -396,7 +400,14 @@ def main():
         if world > 1:
             s.allreduce([0.0])
 
-    phase(rank, f"sweeps: {a.warmup} warmup + {a.steps} timed ({s.smooth_kernel_name(0)})")
+    # settle (untimed, the same count on every rank: rank sweeps exchange halos): ~settle_ms of sweeps
+    # at the fused sweep's ~1.2 ms per 512^3 voxels
+    est_ms = 1.2 * float(shape[0] * shape[1] * shape[2]) / float(512 ** 3)
+    settle = min(2000, max(8, int(math.ceil(a.settle_ms / max(est_ms, 1e-3))))) if a.settle_ms > 0 else 0
+    settle += settle % 2  # even: the ping-pong pair back where setup left it
+    phase(rank, f"sweeps: {settle} settle + {a.warmup} warmup + {a.steps} timed ({s.smooth_kernel_name(0)})")
+    if settle:
+        s.bench_smooth(0, settle)
     # warmup
     if a.warmup:
         s.bench_smooth(0, a.warmup)
@@ -475,6 +486,7 @@ def main():
         "n_gpus": n_gpus,
         "steps": a.steps,
         "warmup": a.warmup,
+        "settle_sweeps": settle,
         "ms_per_step": round(wall / a.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "strong",
