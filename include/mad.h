@@ -199,11 +199,6 @@ typedef struct mad_desc {
 #define MAD_OPT_BENCHMARK_TRACE 16u
 /* MAD_OPT_NO_PLACEMENT_TUNE: keep level 0's first ping-pong allocation (mad_placement_trials; the A/B) */
 #define MAD_OPT_NO_PLACEMENT_TUNE 32u
-/* MAD_OPT_NO_PEER_FOLD: with MAD_OPT_PEER_HALO, take a fused sweep's input ghost planes in with the
-   unpack launch (peer_unpack_k) instead of the sweep's edge workgroups reading them straight from the
-   mailbox.  The fold is used where every rank has a GPU of its own (RCCL, PCI bus ids compared at setup)
-   or stands in for its neighbours (SOLO); identical results */
-#define MAD_OPT_NO_PEER_FOLD 64u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

@@ -36,7 +36,6 @@ OPT_PEER_HALO = 4
 OPT_COARSE_NO_CHAIN = 8
 OPT_BENCHMARK_TRACE = 16  # the reference's -DBENCHMARK history in mad_get_cycle_trace (include/mad.h)
 OPT_NO_PLACEMENT_TUNE = 32  # keep level 0's first allocation (mad_placement_trials)
-OPT_NO_PEER_FOLD = 64  # peer halo: unpack launch before a fused sweep instead of the in-sweep fold
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (

@@ -261,9 +261,6 @@ class Comm {
   }
   // SOLO / RCCL-SOLO: the rank's own arrays stand in for its neighbours'
   bool stand_in() const { return mode_ == SOLO || (mode_ == RCCL && self_); }
-  // RCCL: every rank runs on a device of its own (PCI bus ids all-gathered by share_window); false
-  // before the first share_window and where two ranks share a GPU (the one-GPU multi-process tests)
-  bool distinct_devices() const { return distinct_; }
   // RCCL peer of neighbour rank q (RCCL-SOLO: every peer is this process's only rank)
   int peer(int q) const { return self_ ? 0 : (q + nranks_) % nranks_; }
   Mode mode() const { return mode_; }
@@ -520,43 +517,25 @@ class Comm {
     settle(s);
     // a handle this rank cannot export still takes part in the gather (zeros) and votes no below,
     // so no rank is left waiting in a collective the others skipped
-    // per rank: its window's IPC handle, then its device's PCI bus id (distinct_devices)
-    constexpr size_t BUS = 32;
-    const size_t hb = sizeof(hipIpcMemHandle_t);
-    const size_t rb = hb + BUS;
-    std::vector<char> rec(rb, 0);
     hipIpcMemHandle_t mine;
     std::memset(&mine, 0, sizeof mine);
     bool ok = hipIpcGetMemHandle(&mine, base) == hipSuccess;
     if (!ok) (void)hipGetLastError();
-    std::memcpy(rec.data(), &mine, hb);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(rec.data() + hb, (int)BUS - 1, dev) != hipSuccess) {
-      (void)hipGetLastError();
-      std::memset(rec.data() + hb, 0, BUS);
-    }
-    std::vector<char> all(rb * nranks_);
+    const size_t hb = sizeof(hipIpcMemHandle_t);
+    std::vector<char> all(hb * nranks_);
     char* d = nullptr;
-    HIPC_CHECK(hipMalloc(&d, rb * (nranks_ + 1)));
-    HIPC_CHECK(hipMemcpyAsync(d + rb * nranks_, rec.data(), rb, hipMemcpyHostToDevice, s));
-    NCCL_CHECK(ncclAllGather(d + rb * nranks_, d, rb, ncclChar, comm_, s));
-    HIPC_CHECK(hipMemcpyAsync(all.data(), d, rb * nranks_, hipMemcpyDeviceToHost, s));
+    HIPC_CHECK(hipMalloc(&d, hb * (nranks_ + 1)));
+    HIPC_CHECK(hipMemcpyAsync(d + hb * nranks_, &mine, hb, hipMemcpyHostToDevice, s));
+    NCCL_CHECK(ncclAllGather(d + hb * nranks_, d, hb, ncclChar, comm_, s));
+    HIPC_CHECK(hipMemcpyAsync(all.data(), d, hb * nranks_, hipMemcpyDeviceToHost, s));
     HIPC_CHECK(hipStreamSynchronize(s));
     HIPC_CHECK(hipFree(d));
-    // every rank on a device of its own: each bus id known and no two equal (the same on every rank)
-    distinct_ = true;
-    for (int r = 0; r < nranks_ && distinct_; ++r) {
-      const char* br = all.data() + rb * r + hb;
-      if (!br[0]) distinct_ = false;
-      for (int q = 0; q < r && distinct_; ++q)
-        if (std::strncmp(br, all.data() + rb * q + hb, BUS) == 0) distinct_ = false;
-    }
     // a neighbour's window this process cannot map (no peer access between the two GPUs) makes
     // every rank give the windows up together -- the caller falls back to the exchange -- instead
     // of one rank throwing while the others wait in their next collective
     auto open = [&](int r, void** p) {
       hipIpcMemHandle_t h;
-      std::memcpy(&h, all.data() + rb * r, hb);
+      std::memcpy(&h, all.data() + hb * r, hb);
       if (hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
         (void)hipGetLastError();
         *p = nullptr;
@@ -647,7 +626,6 @@ class Comm {
   int nranks_ = 1;
   int rank_ = 0;
   bool self_ = false;
-  bool distinct_ = false;  // distinct_devices()
   bool graph_pending_ = false;        // a graph with RCCL operations may still be running
   hipStream_t graph_stream_ = nullptr;
 };

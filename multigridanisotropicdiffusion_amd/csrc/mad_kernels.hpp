@@ -434,21 +434,6 @@ struct PeerOut {
   T* dst[2];
   uint32_t* sig[2];
 };
-// Peer halo, consumer side folded into the sweep (PeerIn, round 6): an edge chunk whose input's ghost
-// planes are still in this rank's mailbox (the neighbour's last sweep put them there) reads them from
-// the mailbox instead of the input array -- no unpack launch before the sweep.  Its workgroups wait for
-// the neighbour's count (expect tiles; bounded by tmo, a timeout sets *err as peer_unpack_k does) before
-// their first plane load, and the last of a side's nwg workgroups to pass their edge planes resets that
-// side's counter (ticket[side] counts them).  src[side] null: that side's ghost planes are in the input.
-template <typename T>
-struct PeerIn {
-  const T* src[2];
-  uint32_t* cnt[2];
-  uint32_t* ticket[2];
-  uint32_t* err;
-  uint32_t expect, nwg;
-  uint64_t tmo;
-};
 
 //
 // BL (dense b, not BREC): b is staged through LDS like u -- one coalesced load of the tile region's
@@ -467,8 +452,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
                                                         int zbase, int zstride, int flip_last,
-                                                        uint32_t* __restrict__ sig, PeerOut<T> po,
-                                                        PeerIn<T> pi) {
+                                                        uint32_t* __restrict__ sig, PeerOut<T> po) {
   constexpr int NC = (KIND == KFULL) ? 4 : 2;
   using FG = FusedGeom<NC, TX, TY>;
   constexpr int H = FG::H, RX = FG::RX, RY = FG::RY, HALF = FG::HALF, PITCH = FG::PITCH;
@@ -539,29 +523,6 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   T* const pdst = PEER ? po.dst[flip ? 1 : 0] : nullptr;
   uint32_t* const psig = PEER ? po.sig[flip ? 1 : 0] : (sig ? sig + (flip ? 1 : 0) : nullptr);
   const bool signals = (PEER ? pdst != nullptr : sig != nullptr) && z0 == 0 && zlo_g;
-  // PeerIn: this edge chunk's (logical) lower ghost planes from the mailbox, plane m < 0 at gsrc + m * sz
-  const int pside = flip ? 1 : 0;
-  const T* gsrc = nullptr;
-  if constexpr (PEER) {
-    if (pi.src[pside] != nullptr && z0 == 0 && zlo_g) {
-      __shared__ int pfail;
-      if (tid == 0) {
-        int f = __hip_atomic_load(pi.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
-        const uint64_t t0 = wall_clock64();
-        while (!f && __hip_atomic_load(pi.cnt[pside], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < pi.expect) {
-          __builtin_amdgcn_s_sleep(2);
-          if (wall_clock64() - t0 > pi.tmo) {
-            __hip_atomic_store(pi.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            f = 1;
-          }
-        }
-        pfail = f;
-      }
-      __syncthreads();
-      // (a timed-out wait sweeps on the input's stale ghost planes; the run fails on the sticky error)
-      if (!pfail) gsrc = flip ? pi.src[1] - g.sz : pi.src[0] + (int64_t)GHOST * g.sz;
-    }
-  }
   // first step with its plane parity normalised to even (global z), last step
   const int kbeg = (z0 - (NC - 1)) - ((z0 - (NC - 1) + zpar) & 1);
   const int kend = z1 + NC - 2;
@@ -692,9 +653,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       for (int e = 0; e < UPT; ++e) up[e] = T(0);
     } else {
       m = min(max(m, zlo), zhi - 1);
-      const T* src = uin;
-      if constexpr (PEER) src = (gsrc != nullptr && m < 0) ? gsrc : uin;
-      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(src + (int64_t)m * sz);
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(uin + (int64_t)m * sz);
 #pragma unroll
       for (int e = 0; e < UPT; ++e) up[e] = buf_load<T>(rs, usrc[e], 0u);
     }
@@ -860,21 +819,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
               // this sweep's dirty output) once per tile: 0.30 vs 0.20 ms per 64-plane rank sweep
               __builtin_amdgcn_s_waitcnt(0);
               __syncthreads();
-              if (tid == 0) {
-                if (gsrc != nullptr) {
-                  // this workgroup is past its mailbox planes (loaded, consumed, vmcnt 0): the last one of
-                  // the side resets the side's counter -- before its own count-in below, which the
-                  // neighbour's next sweep into this buffer waits for
-                  const uint32_t tk =
-                      __hip_atomic_fetch_add(pi.ticket[pside], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  if (tk == pi.nwg - 1) {
-                    __hip_atomic_store(pi.cnt[pside], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store(pi.ticket[pside], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  }
-                  __builtin_amdgcn_s_waitcnt(0);
-                }
-                __hip_atomic_fetch_add(psig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              }
+              if (tid == 0) __hip_atomic_fetch_add(psig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
               __threadfence();
               __syncthreads();

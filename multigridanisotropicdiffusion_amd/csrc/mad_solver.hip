@@ -751,33 +751,6 @@ class Solver final : public SolverBase {
                        (uint64_t)bytes, peer_ctl(L.win, L), buf * 2, L.peer_tiles, peer_timeout_ticks_);
     HIP_CHECK(hipGetLastError());
   }
-  // PeerIn of level L's batch in mailbox buffer `buf` (peer_resolve's mailboxes, counters and tile
-  // count; tickets 10 + side of the control block)
-  PeerIn<T> peer_in(LevelData<T>& L, int buf) const {
-    PeerIn<T> p{};
-    uint32_t* ctl = peer_ctl(L.win, L);
-    for (int side = 0; side < 2; ++side) {
-      const bool has = side == 0 ? L.g.zlo_ghost : L.g.zhi_ghost;
-      p.src[side] = has ? mailbox(L.win, L, buf, side) : nullptr;
-      p.cnt[side] = ctl + buf * 2 + side;
-      p.ticket[side] = ctl + 10 + side;
-    }
-    p.err = ctl + 5;
-    p.expect = L.peer_tiles;
-    int tiles = 0, nchunks = 0;
-    fused_shape(L, &tiles, &nchunks);
-    p.nwg = (uint32_t)tiles;  // an edge chunk: one workgroup per tile
-    p.tmo = peer_timeout_ticks_;
-    return p;
-  }
-  // the fold waits inside the sweep's edge workgroups, which could keep a neighbour's sweep sharing the
-  // device off the CUs: only where every rank has a device of its own (RCCL) or stands in for its
-  // neighbours (SOLO, RCCL-SOLO); MAD_OPT_NO_PEER_FOLD keeps the unpack launch
-  bool peer_fold_ok() const {
-    if (c_->d.options & MAD_OPT_NO_PEER_FOLD) return false;
-    if (c_->comm.stand_in()) return true;
-    return c_->comm.mode() == Comm::RCCL && c_->comm.distinct_devices();
-  }
   void peer_resolve_all() {
     for (size_t l = 0; l < lv_.size(); ++l) {
       peer_resolve((int)l);
@@ -1026,7 +999,7 @@ class Solver final : public SolverBase {
   }
 
   template <int KD, int TX, int TY, int NT>
-  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part, bool zu = false, const PeerIn<T>* pin = nullptr) {
+  void launch_fused(LevelData<T>& L, const FusedCfg& fc, int part, bool zu = false) {
     const int ntx = (L.g.nx + TX - 1) / TX, nty = (L.g.ny + TY - 1) / TY;
     const int tiles = ntx * nty;
     int flip = 0;
@@ -1047,7 +1020,6 @@ class Solver final : public SolverBase {
     // which is all its LDS allows anyway)
     constexpr int MW = sizeof(T) == 8 ? 2 : 4;
     const PeerOut<T> po = part == 4 ? peer_out(L, buffer_index(L, L.t)) : PeerOut<T>{{nullptr, nullptr}, {nullptr, nullptr}};
-    const PeerIn<T> pi = pin ? *pin : PeerIn<T>{};
     auto run = [&](auto kern) {
       // every instance that can be launched gets its dynamic-LDS opt-in (a kernel pointer
       // set, not one flag per function type: several instances share one signature)
@@ -1058,7 +1030,7 @@ class Solver final : public SolverBase {
         attr.push_back((const void*)kern);
       }
       hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, po, pi);
+                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, po);
     };
     if (part == 4) {
       if (L.brec)
@@ -1109,17 +1081,17 @@ class Solver final : public SolverBase {
     *nchunks = whole_range(L.g.nz, *tiles, fc).nchunks;
   }
 
-  void launch_fused_part(LevelData<T>& L, int part, bool zu = false, const PeerIn<T>* pin = nullptr) {
+  void launch_fused_part(LevelData<T>& L, int part, bool zu = false) {
     const FusedCfg fc = fused_cfg();
     if (c_->kind == KFULL) {
       if constexpr (sizeof(T) == 4)
-        launch_fused<KFULL, 64, MAD_FUSED_F32_TY, MAD_FUSED_F32_TY * 32>(L, fc, part, zu, pin);
+        launch_fused<KFULL, 64, MAD_FUSED_F32_TY, MAD_FUSED_F32_TY * 32>(L, fc, part, zu);
       else
-        launch_fused<KFULL, 64, 16, 512>(L, fc, part, zu, pin);
+        launch_fused<KFULL, 64, 16, 512>(L, fc, part, zu);
     } else if (c_->kind == KDIAG) {
-      launch_fused<KDIAG, 64, 16, 1024>(L, fc, part, zu, pin);
+      launch_fused<KDIAG, 64, 16, 1024>(L, fc, part, zu);
     } else {
-      launch_fused<KISO, 64, 16, 1024>(L, fc, part, zu, pin);
+      launch_fused<KISO, 64, 16, 1024>(L, fc, part, zu);
     }
     HIP_CHECK(hipGetLastError());
   }
@@ -1216,13 +1188,6 @@ class Solver final : public SolverBase {
   // counters).
   float fused_sweep(int l, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     LevelData<T>& L = lv_[l];
-    // the input's ghost planes still in the mailbox: the sweep's edge chunks read them there (peer_fold)
-    PeerIn<T> pin{};
-    const bool fold = L.peer && L.x_peer_pending && peer_fold_ok();
-    if (fold) {
-      pin = peer_in(L, L.peer_buf);
-      L.x_peer_pending = false;  // consumed by this sweep, which also resets the counters
-    }
     halo(l, L.x, GHOST);
     if (L.brec) {
       sync_brec(l);
@@ -1233,7 +1198,7 @@ class Solver final : public SolverBase {
     if (L.peer) {
       // the sweep delivers its edge planes to the neighbours itself; no exchange follows
       L.peer_buf = buffer_index(L, L.t);
-      launch_fused_part(L, 4, false, fold ? &pin : nullptr);
+      launch_fused_part(L, 4);
       if (e1) HIP_CHECK(hipEventRecord(e1, c_->stream));
       std::swap(L.x, L.t);
       std::swap(L.alloc[0], L.alloc[3]);
@@ -3176,7 +3141,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
     REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO |
                             MAD_OPT_COARSE_NO_CHAIN | MAD_OPT_BENCHMARK_TRACE |
-                            MAD_OPT_NO_PLACEMENT_TUNE | MAD_OPT_NO_PEER_FOLD)) == 0,
+                            MAD_OPT_NO_PLACEMENT_TUNE)) == 0,
             MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");

@@ -421,40 +421,3 @@ def test_filter_run_rank_slabs_bitwise(cycle, precision, peer, in_dtype, nranks)
     assert cycle == 2 or rst["last_relres"] <= 1e-10
     np.testing.assert_array_equal(np.concatenate([o[0] for o in outs]), ref)
     assert all(list(o[1]["step_cycles"]) == list(rst["step_cycles"]) for o in outs)
-
-
-@pytest.mark.parametrize("rank", [0, 2, 3])
-@pytest.mark.parametrize("mode", ["solo", "rccl_solo"])
-def test_peer_fold_equals_unpack(rank, mode):
-    """Round 6: a fused sweep whose input's ghost planes are still in the mailbox reads them there from
-    its edge workgroups (the fold; the last workgroup of a side resets its counter) instead of an unpack
-    launch before it.  Against MAD_OPT_NO_PEER_FOLD (the unpack launch) on the same transport: sweeps
-    (odd and even counts), graph-replayed V-cycles and FMG give the same bits on every level, and every
-    wait is met (a timed-out one fails the download's peer check)."""
-    import multigridanisotropicdiffusion_amd as M
-    from multigridanisotropicdiffusion_amd import distributed as D
-    shape = (128, 64, 64)
-    z0, z1 = D.slabs(shape, 4)[rank]
-    out = {}
-    for fold in (True, False):
-        opts = M.capi.OPT_PEER_HALO | (0 if fold else M.capi.OPT_NO_PEER_FOLD)
-        s = M.Solver((z1 - z0,) + shape[1:], time_step=0.3, nranks=4, rank=rank, global_shape=shape,
-                     min_slab_voxels=DEEP, options=opts, gs_kernel=3)
-        s.comm_init_solo() if mode == "solo" else s.comm_init_rccl_solo()
-        s.synth_tensor(kind=0, seed=9)
-        s.setup()
-        assert "peer halo" in s.smooth_kernel_name(0)
-        s.synth_level(0, M.capi.B, 3)
-        s.synth_level(0, M.capi.X, 4)
-        s.smooth(0, 3)
-        for _ in range(3):
-            s.vcycle()
-        s.smooth(0, 2)
-        s.vcycle()
-        s.fmg()
-        out[fold] = [(s.download(l, M.capi.X), s.download(l, M.capi.B)) for l in range(s.num_levels)]
-        s.close()
-    for l, ((xa, ba), (xb, bb)) in enumerate(zip(out[True], out[False])):
-        assert np.isfinite(xa).all()
-        np.testing.assert_array_equal(xa, xb, err_msg=f"x, level {l}")
-        np.testing.assert_array_equal(ba, bb, err_msg=f"b, level {l}")
