@@ -442,12 +442,16 @@ struct PeerOut {
 // which on the x-parity-interleaved dense b is a stride-2 access (two cache lines per wave load for
 // one line's worth of values).  The LDS then holds NP + NC planes (fp32 64 x 32 tiles: 155 KB).
 //
+// BS (b split, round 6): dense b's values in the records' x-parity-split order (LevelData::bs, cidx), so a
+// stage's b values are one contiguous run per row like its records -- one stride-1 load per stage point,
+// no LDS ring (BL's 62 KB) and no stride-2 access; the copy is refreshed when b changes (sync_bsplit).
+//
 // ZU (zero iterate): the sweep's input u is known to be zero (the first sweep of a correction cycle
 // whose x was zeroed, or never written, by the step before): its planes enter the LDS ring as
 // zeros instead of being loaded -- the same arithmetic on the same values, without the read, and
 // without the zero fill the caller would otherwise write first.
 template <typename T, int KIND, int TX, int TY, int NT, int MINW, int LEAD = 2, bool BREC = false,
-          bool PEER = false, bool BL = false, bool ZU = false>
+          bool PEER = false, bool BL = false, bool ZU = false, bool BS = false>
 __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ uin, T* __restrict__ uout,
                                                         const T* __restrict__ b, const T* __restrict__ cf,
                                                         Geo g, Rat<T> rat, int zc, int ntx, int nty,
@@ -465,6 +469,7 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
   static_assert(TX % 2 == 0 && TY % 2 == 0 && (H % 2) == 0, "even tile geometry");
   static_assert(FG::rows(0) * FG::cols(0) <= NT, "one stage point per thread");
   static_assert(!(BL && BREC), "b rides in the record");
+  static_assert(!(BS && (BL || BREC)), "one form of b");
   constexpr int NB = BL ? NC : 0;  // b ring slots (after the NP u slots)
   extern __shared__ __align__(16) unsigned char fused_smem[];
 
@@ -674,7 +679,9 @@ __global__ void __launch_bounds__(NT, MINW) gs_fused3_k(const T* __restrict__ ui
       const PD d = pdelta(c, PM);
       buf_load_rec<T, RS>(buf_rsrc(cf + ((int64_t)m * sz + cbase + d.g) * RS), pg[c][PM % NPM],
                           raw[c]);
-      if constexpr (!BREC && !BL)
+      if constexpr (BS)  // the split copy: the record's index, stride 1 (pg / RS)
+        bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + cbase + d.g), pg[c][PM % NPM] / (uint32_t)RS, 0u);
+      else if constexpr (!BREC && !BL)
         bv[c] = buf_load<T>(buf_rsrc(b + (int64_t)m * sz + bbase + d.b), pb[c][PM % NPM], 0u);
     }
   };
@@ -1077,7 +1084,8 @@ __global__ void __launch_bounds__(256) residual_k(const T* __restrict__ u, const
 // correction -- and the owned points' u + ue go to uo (a second buffer: neighbouring tiles still
 // read u); xe is then written by a separate fill, since those tiles also read ue.
 // TB: the storage type of b -- float where the refine rhs is an exactly-fp32 image (an 8/16-bit or fp32
-// input in its first time step): read as T, the same values in half the bytes.
+// input in its first time step): read as T, the same values in half the bytes.  bse: be's values also in
+// the records' x-parity-split order (the fused sweep's split copy of b, gs_fused3_k BS).
 template <typename T, int KIND, int TX, int TY, bool BREC = false, typename TE = T, typename TB = T>
 __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, const TB* __restrict__ b,
                                                     T* __restrict__ r, const T* __restrict__ cf,
@@ -1086,7 +1094,8 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
                                                     TE* __restrict__ be = nullptr,
                                                     TE* __restrict__ xe = nullptr,
                                                     const TE* __restrict__ ue = nullptr,
-                                                    T* __restrict__ uo = nullptr) {
+                                                    T* __restrict__ uo = nullptr,
+                                                    TE* __restrict__ bse = nullptr) {
   constexpr int NT = TX * TY;
   constexpr int RX = TX + 2, RY = TY + 2, PL = RX * RY;
   constexpr int UPT = (PL + NT - 1) / NT;
@@ -1203,6 +1212,7 @@ __global__ void __launch_bounds__(TX * TY) resid3_k(const T* __restrict__ u, con
       if (be) {
         const int64_t p = (int64_t)m * sz + pbase + ty * sy + tx;
         be[p] = (TE)rv;
+        if (bse) bse[(int64_t)m * sz + rbase + rec_off / (TS * RS)] = (TE)rv;
         if (xe) xe[p] = TE(0);
         if (uo) uo[p] = P0[0];
       }
@@ -1869,6 +1879,16 @@ __global__ void __launch_bounds__(TX * TY) interp3_k(const T* __restrict__ coars
 
 // copy the dense rhs into the b slot (index ncf) of the coefficient records of local
 // planes [p0, p1) (ghost planes included on rank slabs): LevelData::brec levels
+// dense b -> its x-parity-split copy (gs_fused3_k BS): the records' point order without the stride
+template <typename T>
+__global__ void __launch_bounds__(256) bsplit_k(const T* __restrict__ b, T* __restrict__ bs, Geo g, int p0) {
+  const int k = p0 + (int)blockIdx.z;
+  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.nx || j >= g.ny) return;
+  bs[cidx(g, i, j, k)] = b[i + g.sy * j + g.sz * (int64_t)k];
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) brec_scatter_k(const T* __restrict__ b, T* __restrict__ cf,
                                                       Geo g, int ncf, int p0) {

@@ -292,6 +292,11 @@ struct LevelData {
   T* t = nullptr;  // WJ ping-pong / scratch
   T* cf = nullptr;        // field 0, plane 0 (ghost planes precede it on rank slabs)
   T* cf_alloc = nullptr;
+  // level 0 of the V-cycle layout (fp32, fused): b in the records' x-parity-split order for the sweep
+  // (gs_fused3_k BS), refreshed from the dense b -- the canonical copy -- by sync_bsplit when b changed
+  // (brec_ok doubles as its flag: a level has records carrying b or this copy, never both)
+  T* bs = nullptr;
+  T* bs_alloc = nullptr;
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -339,6 +344,11 @@ struct LevelData {
 // z-depth of a rank slab's boundary chunks (>= GHOST; 4 measured 0.231 vs 0.228 ms per 8-rank
 // sweep, profiles/r02_slab_tiles.log)
 constexpr int BOUNDARY_PLANES = 8;
+// level 0 of the V-cycle layout reads b from an x-parity-split copy (gs_fused3_k BS) instead of staging
+// the dense b through LDS (BL); 0 keeps BL (A/B, profiles/r06_bsplit_ab.log)
+#ifndef MAD_FUSED_B_SPLIT
+#define MAD_FUSED_B_SPLIT 1
+#endif
 inline int boundary_planes() { return BOUNDARY_PLANES; }
 
 template <typename T>
@@ -407,6 +417,11 @@ class Solver final : public SolverBase {
       // it saves (VED diffusion 126 -> 116.5 ms without it, profiles/r01_brec_ab.log).
       // (L.brec / L.g.rs are set above, before the allocation)
       L.cf = L.cf_alloc + cmargin + cgp * cplane;
+      if (l == 0 && dim == 3 && !L.brec && sizeof(T) == 4 && MAD_FUSED_B_SPLIT) {
+        level_alloc((void**)&L.bs_alloc, sizeof(T) * tot);
+        HIP_CHECK(hipMemsetAsync(L.bs_alloc, 0, sizeof(T) * tot, c->stream));
+        L.bs = L.bs_alloc + margin + L.ghost;
+      }
       dim3 gr = grid_for(L.g.nx, L.g.ny, L.g.nz, BLK);
       part_need = std::max<int64_t>(part_need, (int64_t)gr.x * gr.y * gr.z);
     }
@@ -1029,24 +1044,32 @@ class Solver final : public SolverBase {
                                       (int)lds));
         attr.push_back((const void*)kern);
       }
-      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.b, L.cf, L.g, L.rat,
-                         zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, po);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), lds, c_->stream, L.x, L.t, L.bs ? L.bs : L.b, L.cf, L.g,
+                         L.rat, zr.zc, ntx, nty, zr.zbase, zr.zstride, flip, sig, po);
     };
     if (part == 4) {
       if (L.brec)
         run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true, true>);
-      else if constexpr (bl_fits)
-        bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true, true>)
-           : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>);
-      else
+      else if constexpr (bl_fits) {
+        if (L.bs)
+          run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true, false, false, true>);
+        else
+          bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true, true>)
+             : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>);
+      } else
         run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, true>);
     } else if (L.brec) {
       run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, true>);
     } else if constexpr (bl_fits) {
       if (zu) {  // zero iterate (zero_sweep_ok: fp32 whole-slab sweeps only)
         REQUIRE(part == 0, MAD_ERR_STATE, "zero-iterate sweep on a rank slab");
-        bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true, true>)
-           : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, false, true>);
+        if (L.bs)
+          run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, false, true, true>);
+        else
+          bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true, true>)
+             : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, false, true>);
+      } else if (L.bs) {
+        run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, false, false, true>);
       } else {
         bl ? run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2, false, false, true>)
            : run(gs_fused3_k<T, KD, TX, TY, NT, MW, 2>);
@@ -1065,7 +1088,7 @@ class Solver final : public SolverBase {
   // (level 0 only: 1249.7 vs 1279.6 us per 512^3 launch, but 195.7 vs 190.8 us at 256^3,
   // profiles/r04_bl_ab.md)
   bool fused_b_lds(const LevelData<T>& L) const {
-    return MAD_FUSED_B_LDS && sizeof(T) == 4 && !L.brec && &L == &lv_[0];
+    return MAD_FUSED_B_LDS && sizeof(T) == 4 && !L.brec && !L.bs && &L == &lv_[0];
   }
 
   // fp32 full-tensor fused tiles: 64 x 32 in 1024 threads (A/B knob: 16 -> 64 x 16 in 512 threads,
@@ -1118,11 +1141,11 @@ class Solver final : public SolverBase {
       const int nt = (kind == KFULL && sizeof(T) == 8) ? 512 : (kind == KFULL ? MAD_FUSED_F32_TY * 32 : 1024);
       const bool brec = lv_[l].brec;
       const LevelData<T>& L = lv_[l];
-      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER, BL, ZU last; the
+      // every template argument, as rocprofv3 prints the instantiation (BREC, PEER, BL, ZU, BS last; the
       // zero-iterate form is only the first sweep of a refine correction cycle)
-      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s, %s, false>", tn, kind, tx, ty,
-                    nt, sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false", L.peer ? "true" : "false",
-                    fused_b_lds(L) ? "true" : "false");
+      std::snprintf(buf, sizeof buf, "gs_fused3_k<%s, %d, %d, %d, %d, %d, 2, %s, %s, %s, false, %s>", tn, kind, tx,
+                    ty, nt, sizeof(T) == 8 ? 2 : 4, brec ? "true" : "false", L.peer ? "true" : "false",
+                    fused_b_lds(L) ? "true" : "false", L.bs ? "true" : "false");
       // rank slabs: which sweep form fused_sweep takes
       if (L.peer) return std::string(buf) + " [rank slab: peer halo, edge planes stored by the sweep]";
       if (sweep_overlap(l)) {
@@ -1152,6 +1175,21 @@ class Solver final : public SolverBase {
     }
     dim3 gr = grid_for(L.g.nx, L.g.ny, p1 - p0, BLK);
     hipLaunchKernelGGL((brec_scatter_k<T>), gr, BLK, 0, c_->stream, L.b, L.cf, L.g, ncoef_, p0);
+    HIP_CHECK(hipGetLastError());
+    L.brec_ok = true;
+  }
+  // the fused sweep's split copy of b (LevelData::bs), ghost planes included on rank slabs
+  void sync_bsplit(int l) {
+    LevelData<T>& L = lv_[l];
+    if (!L.bs || L.brec_ok) return;
+    int p0 = 0, p1 = L.g.nz;
+    if (c_->comm.active() && c_->geom[l].distributed) {
+      b_halo(l);
+      if (L.g.zlo_ghost) p0 = -GHOST;
+      if (L.g.zhi_ghost) p1 = L.g.nz + GHOST;
+    }
+    dim3 gr = grid_for(L.g.nx, L.g.ny, p1 - p0, BLK);
+    hipLaunchKernelGGL((bsplit_k<T>), gr, BLK, 0, c_->stream, L.b, L.bs, L.g, p0);
     HIP_CHECK(hipGetLastError());
     L.brec_ok = true;
   }
@@ -1193,6 +1231,7 @@ class Solver final : public SolverBase {
       sync_brec(l);
     } else {
       b_halo(l);
+      sync_bsplit(l);
     }
     if (e0) HIP_CHECK(hipEventRecord(e0, c_->stream));
     if (L.peer) {
@@ -1381,6 +1420,7 @@ class Solver final : public SolverBase {
   // levels of >= 16 x 16 write the fp32 hierarchy's next rhs b = (T) r and x = 0 in the same
   // pass instead of r64 (refine_emitted_; else run_refine converts r64 and fills x)
   bool refine_emitted_ = false;
+  bool refine_emitted_bs_ = false;  // ... and the split copy of b (LevelData::bs) with it
   // fold: u += (double) x (the fp32 cycle's correction) in the same pass -- one GPU, resid3_k levels:
   // the updated iterate goes to the second fp64 buffer (r64_, unused by this path) and the pointers
   // swap; x = 0 is then a separate fill (neighbouring tiles read x while the pass runs)
@@ -1439,6 +1479,10 @@ class Solver final : public SolverBase {
       chunks = (g.nz + zc - 1) / zc;
       nparts = (int64_t)ntx * nty * chunks;
       REQUIRE(nparts <= part_cap_, MAD_ERR_UNSUPPORTED, "residual partials buffer too small");
+      // one GPU: the fused sweep's split copy of b written in the same pass (rank slabs refresh it,
+      // ghost planes included, from the dense b: sync_bsplit)
+      T* const bse = (L.bs && !c_->geom[0].distributed) ? L.bs : nullptr;
+      refine_emitted_bs_ = bse != nullptr;
       auto go = [&](auto K) {
         constexpr int KD = decltype(K)::value;
         auto launch = [&](auto bptr) {
@@ -1446,11 +1490,11 @@ class Solver final : public SolverBase {
           if (fold)
             hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T, TB>), dim3((unsigned)nparts),
                                dim3(TX * TY), 0, c_->stream, u64_, bptr, (double*)nullptr, cf64_, g, rat64_, zc,
-                               ntx, part_, L.b, (T*)nullptr, (const T*)L.x, r64_);
+                               ntx, part_, L.b, (T*)nullptr, (const T*)L.x, r64_, bse);
           else
             hipLaunchKernelGGL((resid3_k<double, KD, TX, TY, false, T, TB>), dim3((unsigned)nparts),
                                dim3(TX * TY), 0, c_->stream, u64_, bptr, (double*)nullptr, cf64_, g, rat64_, zc,
-                               ntx, part_, L.b, L.x);
+                               ntx, part_, L.b, L.x, (const T*)nullptr, (double*)nullptr, bse);
         };
 #ifdef MAD_NO_B32_RHS  // A/B: always the fp64 rhs
         launch((const double*)b64_);
@@ -1478,7 +1522,7 @@ class Solver final : public SolverBase {
         hipLaunchKernelGGL((residual_k<double, D.value, K.value>), gr, BLK, 0, c_->stream, u64_, b64_,
                            r64_, cf64_, g, rat64_, part_);
       });
-      refine_emitted_ = false;
+      refine_emitted_ = refine_emitted_bs_ = false;
     }
     HIP_CHECK(hipGetLastError());
     return std::sqrt(finish_norm2(nparts, c_->geom[0].distributed));
@@ -1847,6 +1891,7 @@ class Solver final : public SolverBase {
       return;
     }
     sync_brec(0);  // eager: level 0's b changes between cycles (time steps), not inside
+    sync_bsplit(0);
     if (ranks) ranks_graph_entry();
     const bool zu = zero_x0_;  // the graph bakes in the first sweep's zero-iterate form too
     if (vgraph_) {
@@ -2266,7 +2311,8 @@ class Solver final : public SolverBase {
       }
       if (!fp32_phase || (relres > d.tolerance && it < d.max_cycles)) do {  // MAD.hxx:207-246
         if (refine_emitted_) {  // b = (T) r and x = 0 written by residual64's pass
-          L0.b_halo_ok = L0.brec_ok = false;
+          L0.b_halo_ok = false;
+          L0.brec_ok = refine_emitted_bs_;  // the split copy of b too
           x_changed(0);
         } else {
           to_fp32_rhs(r64_);
@@ -2499,6 +2545,7 @@ class Solver final : public SolverBase {
       for (auto& a : L.alloc)
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
+      if (L.bs_alloc) (void)hipFree(L.bs_alloc);
     }
     lv_.clear();
     for (auto& a : r64alloc_)
