@@ -446,9 +446,13 @@ def main():
             s.close()
             s = make(M.VCYCLE, 0, "vcycle-rccl")
     s.vcycle()
+    # untimed cycles as the sweeps' settle phase (same count on every rank: ~settle_ms at ~6 sweeps each)
+    settle_vc = int(math.ceil(settle / 6.0)) if settle else 0
+    if settle_vc:
+        s.bench_vcycle(settle_vc)
     barrier()
     t1 = time.perf_counter()
-    phase(rank, f"V-cycles: {a.vcycles} timed")
+    phase(rank, f"V-cycles: {settle_vc} settle + {a.vcycles} timed")
     vc_ms = s.bench_vcycle(a.vcycles)
     barrier()
     vwall = time.perf_counter() - t1
