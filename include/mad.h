@@ -199,6 +199,9 @@ typedef struct mad_desc {
 #define MAD_OPT_BENCHMARK_TRACE 16u
 /* MAD_OPT_NO_PLACEMENT_TUNE: keep level 0's first ping-pong allocation (mad_placement_trials; the A/B) */
 #define MAD_OPT_NO_PLACEMENT_TUNE 32u
+/* MAD_OPT_NO_RECORD_B: in CycleType SMOOTHER, level 0's records do not carry b (40-B records); the sweep
+   reads b from the split copy the V-cycle layout uses (36-B records + 4 B) -- the A/B of the two forms */
+#define MAD_OPT_NO_RECORD_B 64u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */

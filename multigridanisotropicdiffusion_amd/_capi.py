@@ -36,6 +36,7 @@ OPT_PEER_HALO = 4
 OPT_COARSE_NO_CHAIN = 8
 OPT_BENCHMARK_TRACE = 16  # the reference's -DBENCHMARK history in mad_get_cycle_trace (include/mad.h)
 OPT_NO_PLACEMENT_TUNE = 32  # keep level 0's first allocation (mad_placement_trials)
+OPT_NO_RECORD_B = 64  # SMOOTHER: level-0 records without b (the split-b sweep instead)
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (

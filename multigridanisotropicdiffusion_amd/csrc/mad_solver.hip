@@ -386,7 +386,7 @@ class Solver final : public SolverBase {
       // up to a tile halo outside the outermost (ghost) plane
       const int64_t margin = margin_elems(L.g);
       const int64_t tot = L.g.N + 2 * (L.ghost + margin);
-      bool brec_on = c->d.cycle == MAD_SMOOTHER;
+      bool brec_on = c->d.cycle == MAD_SMOOTHER && !(c->d.options & MAD_OPT_NO_RECORD_B);
       if (c->d.precision == MAD_FP32_REFINE) brec_on = false;  // b changes every cycle there
       L.brec = (dim == 3 && l == 0 && brec_on);
       L.g.rs = ncoef_ + (L.brec ? 1 : 0);
@@ -3188,7 +3188,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
     REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO |
                             MAD_OPT_COARSE_NO_CHAIN | MAD_OPT_BENCHMARK_TRACE |
-                            MAD_OPT_NO_PLACEMENT_TUNE)) == 0,
+                            MAD_OPT_NO_PLACEMENT_TUNE | MAD_OPT_NO_RECORD_B)) == 0,
             MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");

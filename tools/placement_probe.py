@@ -24,6 +24,8 @@ sys.path.insert(0, ROOT)
 
 def sweep_ms(M):
     opt = M.capi.OPT_NO_PLACEMENT_TUNE if os.environ.get("MAD_PROBE_NOTUNE") == "1" else 0
+    if os.environ.get("MAD_PROBE_NORECB") == "1":  # SMOOTHER without b in the records (split-b sweep)
+        opt |= M.capi.OPT_NO_RECORD_B
     cyc = M.VCYCLE if os.environ.get("MAD_PROBE_LAYOUT") == "vcycle" else M.SMOOTHER
     # MAD_PROBE_GSK=4: the last z-chunk marched downward (mad_desc.gs_kernel 4)
     s = M.Solver((512, 512, 512), (1.0, 1.0, 1.0), time_step=0.1, precision=M.FP32, cycle=cyc,
@@ -75,6 +77,10 @@ def places(specs, reps):
             env.pop("MAD_PROBE_NOTUNE", None)
             env.pop("MAD_PROBE_LAYOUT", None)
             env.pop("MAD_PROBE_GSK", None)
+            env.pop("MAD_PROBE_NORECB", None)
+            if spec.startswith("bs"):  # SMOOTHER layout, b from the split copy instead of the records
+                env["MAD_PROBE_NORECB"] = "1"
+                spec = spec[len("bs"):].lstrip("-") or "tune"
             if spec.startswith("flip"):  # gs_kernel 4: the second z-chunk marches downward
                 env["MAD_PROBE_GSK"] = "4"
                 spec = spec[len("flip"):].lstrip("-") or "tune"
