@@ -492,14 +492,15 @@ class Solver final : public SolverBase {
   // other boxes every allocation runs 1.24 ms (profiles/r06_placement.md).  So setup times both
   // directions of the level's own sweep on its arrays and on fresh allocations of them (the pair each
   // time, the records too every second time; contents copied over) and keeps the fastest set, the
-  // others freed: until both directions of the kept set are within 2 % of the fastest direction seen
-  // once the two speeds have shown up, at most PLACEMENT_TRIES sets.  3D levels of >= 2^24 voxels
+  // others freed: at least PLACEMENT_MIN_TRIES sets, then until both directions of the kept set are within
+  // 2 % of the fastest direction seen once a slower speed has shown up, at most PLACEMENT_TRIES sets.  3D levels of >= 2^24 voxels
   // (a rank's slab too: 512 x 512 x 64 on 8 ranks) whose sweep is the fused GS sweep -- timed as the
   // plain whole-slab launch, no exchange, so every rank decides alone -- or, on one rank, the WJ sweep;
   // with the memory for a second set.  Not on the in-process transport (its ranks share one device).
   // MAD_OPT_NO_PLACEMENT_TUNE keeps the first allocation.  Every level of >= 2^24 voxels is tuned so
   // (level 1 of a 512^3 grid too); mad_placement_trials reports level 0's trials.
   static constexpr int PLACEMENT_TRIES = 8;
+  static constexpr int PLACEMENT_MIN_TRIES = 4;
   void tune_placement(int l) {
     if (c_->dim != 3 || (c_->d.options & MAD_OPT_NO_PLACEMENT_TUNE)) return;
     if (c_->comm.active() && c_->comm.mode() == Comm::LOCAL) return;
@@ -568,8 +569,10 @@ class Solver final : public SolverBase {
     double bf = 0.0, br = 0.0;
     time_dirs(&bf, &br);
     for (int tr = 1; tr < PLACEMENT_TRIES; ++tr) {
-      // the kept set is at the fast speed, and a slower one has been seen (so that speed is the fast one)
-      if (slowest > 1.05 * fastest && std::max(bf, br) <= 1.02 * fastest) break;
+      // the kept set is at the fastest speed seen, a slower one has been seen, and at least
+      // PLACEMENT_MIN_TRIES sets were timed (some kernels have three speeds: the split-b sweep
+      // 1.16 / 1.21 / 1.28 ms on one box, profiles/r06_record_b_ab.log)
+      if (tr >= PLACEMENT_MIN_TRIES && slowest > 1.05 * fastest && std::max(bf, br) <= 1.02 * fastest) break;
       const bool with_cf = (tr % 2) == 0;
       size_t free_b = 0, total_b = 0;
       HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
