@@ -22,7 +22,8 @@ def main():
     # the timed cycles are the last `cycles` repetitions; one coarse solve per V-cycle, so the
     # kernels after the (cycles+1)-th last coarse solve up to the last one are `cycles` whole
     # cycles' worth (second half of one, first half of the next)
-    cs = [i for i, e in enumerate(ev) if "coarse_solve" in e[2]]
+    # (with the one-launch V-cycle tail, vtail_k stands in for the coarse solve)
+    cs = [i for i, e in enumerate(ev) if "coarse_solve" in e[2] or "vtail_k" in e[2]]
     sel = ev[cs[-(a.cycles + 1)] + 1: cs[-1] + 1]
     span = (sel[-1][1] - sel[0][0]) / 1e6
     busy = sum(e[1] - e[0] for e in sel) / 1e6

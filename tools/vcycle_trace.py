@@ -39,7 +39,7 @@ def main():
         else:
             s.comm_init_solo()
     else:
-        s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32, cycle=cyc)
+        s = M.Solver((S, S, S), time_step=0.1, precision=M.FP32, cycle=cyc, options=a.options)
     s.synth_tensor(kind=0, seed=4)
     s.setup()
     s.synth_level(0, M.capi.B, 3)
