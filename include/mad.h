@@ -202,10 +202,6 @@ typedef struct mad_desc {
 /* MAD_OPT_NO_RECORD_B: in CycleType SMOOTHER, level 0's records do not carry b (40-B records); the sweep
    reads b from the split copy the V-cycle layout uses (36-B records + 4 B) -- the A/B of the two forms */
 #define MAD_OPT_NO_RECORD_B 64u
-/* MAD_OPT_NO_VCYCLE_TAIL: the small replicated coarse levels (<= 32^3 voxels and everything coarser) run
-   as per-level launches (~19 per level) instead of the one-launch LDS-resident V-cycle tail (vtail_k);
-   identical results -- the A/B of the two forms */
-#define MAD_OPT_NO_VCYCLE_TAIL 128u
 
 typedef struct mad_stats {
   uint32_t steps;                /* time steps run */
@@ -280,10 +276,6 @@ int mad_get_cycle_trace(const mad_ctx *ctx, uint32_t cap, uint32_t *step, double
  * keeping the fastest.  ms receives (forward, reverse) sweep ms per pair tried, in order; *count =
  * 2 x pairs, 0 when nothing was tuned (levels < 2^24 voxels, rank slabs, MAD_OPT_NO_PLACEMENT_TUNE). */
 int mad_placement_trials(const mad_ctx *ctx, uint32_t cap, double *ms, uint32_t *count);
-/* The V-cycle tail a V-cycle entering level `level` would launch (MAD_OPT_NO_VCYCLE_TAIL): its
-   workgroups and dynamic LDS bytes, or *workgroups = 0 when that level runs the per-level launches
-   (distributed / large / fused levels, verbose, WJ or lexicographic smoothers, block-LU coarsest). */
-int mad_vcycle_tail(const mad_ctx *ctx, int32_t level, int32_t *workgroups, int64_t *lds_bytes);
 
 /* ---------------------------------------------------------------- hierarchy */
 int mad_num_levels(const mad_ctx *ctx);               /* GH::GetMaxDepth() + 1 */

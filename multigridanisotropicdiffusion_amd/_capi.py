@@ -37,14 +37,13 @@ OPT_COARSE_NO_CHAIN = 8
 OPT_BENCHMARK_TRACE = 16  # the reference's -DBENCHMARK history in mad_get_cycle_trace (include/mad.h)
 OPT_NO_PLACEMENT_TUNE = 32  # keep level 0's first allocation (mad_placement_trials)
 OPT_NO_RECORD_B = 64  # SMOOTHER: level-0 records without b (the split-b sweep instead)
-OPT_NO_VCYCLE_TAIL = 128  # small coarse levels as per-level launches instead of the one-launch tail (A/B)
 VED_OPT_LINE_WALK = 1
 
 EXPORTS = (
     "mad_desc_init", "mad_max_depth", "mad_create", "mad_destroy", "mad_last_error",
     "mad_get_desc", "mad_set_tensor", "mad_set_tensor_device", "mad_tensor_planes",
     "mad_set_tensor_planes", "mad_setup", "mad_run",
-    "mad_run_device", "mad_get_step_stats", "mad_get_cycle_trace", "mad_placement_trials", "mad_vcycle_tail", "mad_num_levels", "mad_plan_level",
+    "mad_run_device", "mad_get_step_stats", "mad_get_cycle_trace", "mad_placement_trials", "mad_num_levels", "mad_plan_level",
     "mad_level_info", "mad_upload",
     "mad_download", "mad_fill", "mad_smooth", "mad_residual", "mad_norm", "mad_restrict",
     "mad_residual_restrict",
@@ -204,7 +203,6 @@ def load():
         "mad_get_step_stats": ([vp, u32, u32p, dp], i32),
         "mad_get_cycle_trace": ([vp, u32, u32p, dp, dp, u32p], i32),
         "mad_placement_trials": ([vp, u32, dp, u32p], i32),
-        "mad_vcycle_tail": ([vp, i32, i32p, i64p], i32),
         "mad_num_levels": ([vp], i32),
         "mad_plan_level": ([ctypes.POINTER(MadDesc), i32, i64p, dp, i32p, i64p, i64p, i32p], i32),
         "mad_level_info": ([vp, i32, i64p, dp, i32p], i32),

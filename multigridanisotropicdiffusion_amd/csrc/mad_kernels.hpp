@@ -1922,377 +1922,6 @@ __global__ void __launch_bounds__(256) coarse_solve_k(const double* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// V-cycle tail: the small replicated coarse levels of a V-cycle -- from a level l0 (<= 32^3 voxels by
-// default) down to the coarsest and back: nu multicolour GS sweeps, residual + restriction with the
-// coarse x zeroed, the dense coarsest solve, prolongation + add, nu sweeps -- in ONE launch of NWG
-// workgroups, each of which keeps the records, b and x of its own z-planes of every tail level in LDS
-// for the whole launch (plus the two neighbour x planes as ghosts).  Phases are separated by a
-// device-wide barrier (agent-scope release increment / acquire spin); between colour phases only a
-// workgroup's two edge planes go through memory (a two-slot hand-over buffer per level: a neighbour may
-// still read slot p while this workgroup writes slot p + 1).  Every point goes through the same device
-// functions in the same order as the launches it replaces -- gs_color_k per colour, resid_restrict3_k's
-// residual and its x, y, then z restriction chain, coarse_solve_k's row dot product, interp3_k's taps
-// and fma chain -- so the result is bit-identical to them.  Each of those ~19 launches per level costs
-// ~5 us at these sizes; a phase here measured 3.5-6 us (profiles/r06_tail_probe.log): the launch is slower.
-// (itkMultigridAnisotropicDiffusionImageFilter.hxx:341-493, the same recursion as vcycle_rec)
-constexpr int TAIL_MAX_LEVELS = 6;
-template <typename T>
-struct TailLevel {
-  T* x;          // iterate (global): the top level's initial x in; every level's final x out
-  T* b;          // rhs (global): the top level's in; the coarser levels' out (as the launches leave it)
-  const T* cf;   // coefficient records (Geo::rs stride, cidx order)
-  T* xch;        // hand-over between workgroups: 2 slots x N (edge planes per colour phase, the level's
-                 // final x; the coarsest level's b in slot 0 and x in slot 1)
-  Geo g;         // replicated level: sy == nx, sz == nx * ny, zoff == 0
-  Rat<T> rat;
-  int cent[3];
-  int ppw;       // z-planes per workgroup
-  uint32_t lds;  // byte offset of the level's LDS region: x (ppw + 2 planes), b, r, records (ppw each)
-};
-template <typename T>
-struct TailArgs {
-  TailLevel<T> lv[TAIL_MAX_LEVELS];
-  int nlev;            // levels in lv; the last one is the coarsest (dense inverse, no LDS region)
-  int nu;              // sweeps before and after the coarse-grid correction (>= 1)
-  int ncolors;         // 4 (19-point) or 2 (7-point)
-  const double* inv;   // coarsest inverse, row-major n x n
-  T* xy;               // restriction scratch: per fine plane, its x-y restricted residual per coarse column
-  unsigned* sync;      // [0] barrier arrivals, [1] finished workgroups, [2] error (sticky)
-  uint64_t tmo;        // barrier wait bound (wall-clock ticks)
-  uint64_t* stamps;    // probe only (tools/tail_probe.hip): workgroup 0's wall clock at the start, after
-                       // the loads and after every barrier; nullptr in the solver
-};
-
-// global -> LDS copy of n elements: 16-byte vectors where both ends are aligned, 8 loads in flight per thread
-template <typename T>
-__device__ __forceinline__ void tail_copy(T* __restrict__ dst, const T* __restrict__ src, int n, int tid, int nt) {
-  int done = 0;
-  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
-    const int nv = (int)((int64_t)n * (int)sizeof(T) / 16);
-    const uint4* s = reinterpret_cast<const uint4*>(src);
-    uint4* d = reinterpret_cast<uint4*>(dst);
-    for (int e = tid; e < nv; e += 8 * nt) {
-      uint4 r[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (e + u * nt < nv) r[u] = s[e + u * nt];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (e + u * nt < nv) d[e + u * nt] = r[u];
-    }
-    done = (int)((int64_t)nv * 16 / (int)sizeof(T));
-  }
-  for (int e = done + tid; e < n; e += nt) dst[e] = src[e];
-}
-
-// Every value a workgroup reads from another one comes from the hand-over buffers (xch, xy).  (Those in
-// uncached memory with relaxed barriers -- no L2 write-back / invalidation -- gave run-to-run different
-// results: rejected, profiles/r06_tail_probe.log.)
-template <typename T, int KIND>
-__global__ void __launch_bounds__(256) vtail_k(TailArgs<T> a) {
-#pragma clang fp contract(off)  // the transfer formulas' explicit fma (as resid_restrict3_k / interp3_k)
-  constexpr int NCF = CoefLayout<3, KIND>::N;
-  extern __shared__ __align__(16) unsigned char tail_smem[];
-  __shared__ int dead;
-  const int tid = threadIdx.x, nt = blockDim.x, w = blockIdx.x;
-  const unsigned nwg = gridDim.x;
-  if (__hip_atomic_load(a.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;  // sticky
-  if (tid == 0) dead = 0;
-  unsigned arrivals = 0;
-  int ph = 0;                    // hand-over slot parity
-  unsigned fin = 0;              // bit q: the slot of level q's xch holding its final x
-  int nstamp = 0;
-  auto stamp = [&]() {
-    if (a.stamps && w == 0 && tid == 0) a.stamps[nstamp++] = wall_clock64();
-  };
-  stamp();
-  auto grid_sync = [&]() -> bool {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores complete before the release
-    __syncthreads();
-    arrivals += nwg;
-    if (tid == 0) {
-      __hip_atomic_fetch_add(a.sync, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t t0 = wall_clock64();
-      while (__hip_atomic_load(a.sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < arrivals) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > a.tmo) {  // a workgroup never arrived: error, not a hang
-          __hip_atomic_store(a.sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          dead = 1;
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    stamp();
-    return dead == 0;
-  };
-  struct Own {
-    int k0, m, nx, ny, P;
-    T *xs, *bs, *rs, *cs;
-  };
-  auto own = [&](int q) {
-    const TailLevel<T>& L = a.lv[q];
-    Own o;
-    o.nx = L.g.nx;
-    o.ny = L.g.ny;
-    o.P = o.nx * o.ny;
-    o.k0 = min(w * L.ppw, L.g.nz);
-    o.m = min(L.ppw, L.g.nz - o.k0);
-    o.xs = reinterpret_cast<T*>(tail_smem + L.lds);
-    o.bs = o.xs + (L.ppw + 2) * o.P;
-    o.rs = o.bs + L.ppw * o.P;
-    o.cs = o.rs + L.ppw * o.P;
-    return o;
-  };
-  // stencil terms of own point (i, j, k) from the LDS planes (gather_nb's order and mirrors)
-  auto terms = [&](const TailLevel<T>& L, const Own& o, int i, int j, int k, T& D, T& S) {
-    const T* u = o.xs + (k - o.k0 + 1) * o.P + j * o.nx + i;
-    const int dxm = (i == 0) ? 1 : -1, dxp = (i == o.nx - 1) ? -1 : 1;
-    const int dym = (j == 0) ? o.nx : -o.nx, dyp = (j == o.ny - 1) ? -o.nx : o.nx;
-    const int dzm = (k == 0 && !L.g.zlo_ghost) ? o.P : -o.P;
-    const int dzp = (k == L.g.nz - 1 && !L.g.zhi_ghost) ? -o.P : o.P;
-    T nb[18];
-    nb[0] = u[dxp];
-    nb[1] = u[dxm];
-    nb[2] = u[dyp];
-    nb[3] = u[dym];
-    nb[4] = u[dzp];
-    nb[5] = u[dzm];
-    if (KIND == KFULL) {
-      nb[6] = u[dxp + dyp];
-      nb[7] = u[dxp + dym];
-      nb[8] = u[dxm + dyp];
-      nb[9] = u[dxm + dym];
-      nb[10] = u[dxp + dzp];
-      nb[11] = u[dxp + dzm];
-      nb[12] = u[dxm + dzp];
-      nb[13] = u[dxm + dzm];
-      nb[14] = u[dyp + dzp];
-      nb[15] = u[dyp + dzm];
-      nb[16] = u[dym + dzp];
-      nb[17] = u[dym + dzm];
-    }
-    Coefs<T> c;  // records in LDS in their global (cidx, x-parity split) order
-    const int ci = (k - o.k0) * o.P + j * o.nx + ((i & 1) ? L.g.hx0 + (i >> 1) : (i >> 1));
-    coefs_from_raw<T, 3, KIND>(o.cs + ci * NCF, L.rat, c);
-    stencil_combine<T, 3, KIND>(c, nb, D, S);
-  };
-  auto colour = [&](int q, int color) {
-    const TailLevel<T>& L = a.lv[q];
-    const Own o = own(q);
-    const int hx = (o.nx + 1) / 2, rows = (a.ncolors == 4) ? (o.ny + 1) / 2 : o.ny;
-    const int cnt = hx * rows * o.m;
-    for (int e = tid; e < cnt; e += nt) {
-      const int iq = e % hx, t = e / hx, jq = t % rows, k = o.k0 + t / rows;
-      const int kg = k + L.g.zoff;
-      int i, j;
-      if (a.ncolors == 4) {
-        j = 2 * jq + (((color >> 1) ^ kg) & 1);
-        i = 2 * iq + (((color & 1) ^ kg) & 1);
-      } else {
-        j = jq;
-        i = 2 * iq + ((color + j + kg) & 1);
-      }
-      if (i >= o.nx || j >= o.ny) continue;
-      T D, S;
-      terms(L, o, i, j, k, D, S);
-      const int pl = (k - o.k0) * o.P + j * o.nx + i;
-      o.xs[o.P + pl] = gs_update(o.bs[pl], S, D);
-    }
-  };
-  // after a colour phase: the edge planes into hand-over slot s (all own planes into x as well when
-  // `all`: the level's last phase), the barrier, the neighbours' edge planes into the ghost slots
-  auto publish = [&](int q, bool all) {
-    const TailLevel<T>& L = a.lv[q];
-    const Own o = own(q);
-    if (o.m == 0) return;
-    T* X = L.xch + (int64_t)(ph & 1) * L.g.nz * o.P;
-    if (all) {  // the level's final x: the output array, and the hand-over slot for the next finer level
-      for (int e = tid; e < o.m * o.P; e += nt) {
-        L.x[(int64_t)o.k0 * o.P + e] = o.xs[o.P + e];
-        X[(int64_t)o.k0 * o.P + e] = o.xs[o.P + e];
-      }
-      return;
-    }
-    if (o.k0 > 0)
-      for (int e = tid; e < o.P; e += nt) X[(int64_t)o.k0 * o.P + e] = o.xs[o.P + e];
-    if (o.k0 + o.m < L.g.nz)
-      for (int e = tid; e < o.P; e += nt) X[(int64_t)(o.k0 + o.m - 1) * o.P + e] = o.xs[o.m * o.P + e];
-  };
-  auto ghosts = [&](int q) {
-    const TailLevel<T>& L = a.lv[q];
-    const Own o = own(q);
-    if (o.m == 0) return;
-    const T* X = L.xch + (int64_t)(ph & 1) * L.g.nz * o.P;
-    if (o.k0 > 0)
-      for (int e = tid; e < o.P; e += nt) o.xs[e] = X[(int64_t)(o.k0 - 1) * o.P + e];
-    if (o.k0 + o.m < L.g.nz)
-      for (int e = tid; e < o.P; e += nt) o.xs[(o.m + 1) * o.P + e] = X[(int64_t)(o.k0 + o.m) * o.P + e];
-  };
-  // nu sweeps of level q; post: the level's last phase stores all own planes of x (and on the top
-  // level ends the kernel without a barrier).  false: a barrier timed out
-  auto sweeps = [&](int q, bool post) -> bool {
-    for (int s = 0; s < a.nu; ++s)
-      for (int c = 0; c < a.ncolors; ++c) {
-        colour(q, c);
-        __syncthreads();
-        const bool last = post && s == a.nu - 1 && c == a.ncolors - 1;
-        publish(q, last);
-        if (last) fin = (fin & ~(1u << q)) | ((unsigned)(ph & 1) << q);
-        if (last && q == 0) {
-          stamp();
-          return true;
-        }
-        if (!grid_sync()) return false;
-        if (!last) {
-          ghosts(q);
-          __syncthreads();
-        }
-        ++ph;
-      }
-    return true;
-  };
-
-  // the records of every tail level's own planes (one contiguous block each: rs == NCF on these
-  // levels), the top level's b and x (own planes + ghosts): straight copies, 16-B vectors where aligned
-  for (int q = 0; q + 1 < a.nlev; ++q) {
-    const TailLevel<T>& L = a.lv[q];
-    const Own o = own(q);
-    if (o.m == 0) continue;
-    tail_copy(o.cs, L.cf + (int64_t)o.k0 * o.P * NCF, o.m * o.P * NCF, tid, nt);
-    if (q == 0) {
-      tail_copy(o.bs, L.b + (int64_t)o.k0 * o.P, o.m * o.P, tid, nt);
-      const int lo = max(o.k0 - 1, 0), hi = min(o.k0 + o.m, L.g.nz - 1);
-      tail_copy(o.xs + (lo - o.k0 + 1) * o.P, L.x + (int64_t)lo * o.P, (hi - lo + 1) * o.P, tid, nt);
-    }
-  }
-  __syncthreads();
-  stamp();
-
-  // descent
-  for (int q = 0; q + 1 < a.nlev; ++q) {
-    const TailLevel<T>& F = a.lv[q];
-    const TailLevel<T>& C = a.lv[q + 1];
-    if (!sweeps(q, false)) return;
-    // residual of the own planes (resid_value, as resid_restrict3_k) and their x-y restriction
-    const Own o = own(q);
-    for (int e = tid; e < o.m * o.P; e += nt) {
-      const int kl = e / o.P, ij = e - kl * o.P, j = ij / o.nx, i = ij - j * o.nx;
-      T D, S;
-      terms(F, o, i, j, o.k0 + kl, D, S);
-      o.rs[e] = resid_value(o.bs[e], D, o.xs[o.P + e], S);
-    }
-    __syncthreads();
-    const int ncx = C.g.nx, ncy = C.g.ny, PC = ncx * ncy;
-    for (int e = tid; e < o.m * PC; e += nt) {
-      const int kl = e / PC, IJ = e - kl * PC, J = IJ / ncx, I = IJ - J * ncx;
-      int ix[4], iy[4];
-      T wx[4], wy[4];
-      rtaps4<T>(I, ncx, C.cent[0], ix, wx);
-      rtaps4<T>(J, ncy, C.cent[1], iy, wy);
-      const T* pl = o.rs + kl * o.P;
-      T vz = T(0);
-#pragma unroll
-      for (int bq = 0; bq < 4; ++bq) {
-        const T* row = pl + iy[bq] * o.nx;
-        T vy = T(0);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) vy = fma(wx[t], row[ix[t]], vy);
-        vz = fma(wy[bq], vy, vz);
-      }
-      a.xy[(int64_t)(o.k0 + kl) * PC + IJ] = vz;
-    }
-    if (!grid_sync()) return;
-    // the coarse planes: z restriction into b, x zeroed
-    const bool coarsest = q + 2 == a.nlev;
-    int kc0 = 0, mc = 0;
-    T *xc = nullptr, *bc = nullptr;
-    if (coarsest) {
-      mc = (C.g.nz + (int)nwg - 1) / (int)nwg;
-      kc0 = min(w * mc, C.g.nz);
-      mc = min(mc, C.g.nz - kc0);
-    } else {
-      const Own oc = own(q + 1);
-      kc0 = oc.k0;
-      mc = oc.m;
-      xc = oc.xs;
-      bc = oc.bs;
-    }
-    for (int e = tid; e < mc * PC; e += nt) {
-      const int Kl = e / PC, IJ = e - Kl * PC;
-      int iz[4];
-      T wz[4];
-      rtaps4<T>(kc0 + Kl + C.g.zoff, C.g.nz, C.cent[2], iz, wz);
-      T v = T(0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v = fma(wz[c], a.xy[(int64_t)(iz[c] - F.g.zoff) * PC + IJ], v);
-      C.b[(int64_t)(kc0 + Kl) * PC + IJ] = v;
-      if (!coarsest) bc[Kl * PC + IJ] = v;
-      else C.xch[(int64_t)(kc0 + Kl) * PC + IJ] = v;  // slot 0: the solve's b
-    }
-    if (!coarsest) {
-      for (int e = tid; e < (C.ppw + 2) * PC; e += nt) xc[e] = T(0);
-      __syncthreads();
-    } else {
-      if (!grid_sync()) return;
-      // coarsest: x = A^-1 b, one wave per row (coarse_solve_k's reduction)
-      const int n = (int)C.g.N, lane = tid & 63, wpb = nt >> 6;
-      for (int row = w * wpb + (tid >> 6); row < n; row += (int)nwg * wpb) {
-        const double sacc = coarse_row_dot(a.inv + (int64_t)row * n, (const T*)C.xch, n, lane);
-        if (lane == 0) {
-          C.x[row] = (T)sacc;
-          C.xch[n + row] = (T)sacc;  // slot 1: x for the interpolation
-        }
-      }
-      fin |= 1u << (q + 1);
-      if (!grid_sync()) return;
-    }
-  }
-  // ascent: x += P x_coarse on the own planes and the ghost planes (the neighbours add the same), sweeps
-  for (int q = a.nlev - 2; q >= 0; --q) {
-    const TailLevel<T>& F = a.lv[q];
-    const TailLevel<T>& C = a.lv[q + 1];
-    const Own o = own(q);
-    if (o.m > 0) {
-      const int lo = max(o.k0 - 1, 0), hi = min(o.k0 + o.m, F.g.nz - 1);
-      const int ncx = C.g.nx, ncy = C.g.ny, PC = ncx * ncy;
-      for (int e = tid; e < (hi - lo + 1) * o.P; e += nt) {
-        const int kl = e / o.P, ij = e - kl * o.P, j = ij / o.nx, i = ij - j * o.nx, k = lo + kl;
-        int ix[2], iy[2], iz[2];
-        T wx[2], wy[2], wz[2];
-        itaps2<T>(i, ncx, C.cent[0], ix, wx);
-        itaps2<T>(j, ncy, C.cent[1], iy, wy);
-        itaps2<T>(k + F.g.zoff, C.g.nz, C.cent[2], iz, wz);
-        T v = T(0);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const T* pl = C.xch + (int64_t)((fin >> (q + 1)) & 1u) * C.g.N + (int64_t)(iz[c] - C.g.zoff) * PC;
-          T vz = T(0);
-#pragma unroll
-          for (int bq = 0; bq < 2; ++bq) {
-            const T* row = pl + iy[bq] * ncx;
-            vz = fma(wy[bq], fma(wx[1], row[ix[1]], wx[0] * row[ix[0]]), vz);
-          }
-          v = fma(wz[c], vz, v);
-        }
-        T* xp = o.xs + (k - o.k0 + 1) * o.P + ij;
-        *xp = *xp + v;
-      }
-    }
-    __syncthreads();
-    if (!sweeps(q, true)) return;
-  }
-  // the last workgroup out resets the counters for the next launch (stream order: no one spins now)
-  if (tid == 0) {
-    const unsigned d = __hip_atomic_fetch_add(a.sync + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == nwg - 1) {
-      __hip_atomic_store(a.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // elementwise helpers
 template <typename T>
 __global__ void __launch_bounds__(256) fill_k(T* __restrict__ x, int64_t n, T v) {

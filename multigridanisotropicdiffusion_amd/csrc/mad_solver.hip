@@ -269,8 +269,6 @@ struct SolverBase {
   virtual std::string smooth_kernel(int l) = 0;
   // level-0 sweep ms of every placement candidate setup timed (Solver::tune_placement)
   virtual std::vector<double> placement_ms() const { return {}; }
-  // the V-cycle tail's launch shape from level l (Solver::tail_plan); false: per-level launches
-  virtual bool tail_shape(int l, int* nwg, size_t* lds) const { return false; }
 };
 
 mad_ctx::~mad_ctx() {
@@ -299,7 +297,6 @@ struct LevelData {
   // (brec_ok doubles as its flag: a level has records carrying b or this copy, never both)
   T* bs = nullptr;
   T* bs_alloc = nullptr;
-  T* xch = nullptr;  // V-cycle tail (vtail_k): hand-over between its workgroups, 2 x N (small replicated levels)
   Rat<T> rat{};
   int64_t ghost = 0;      // elements of the ghost planes on one side (3D: GHOST * sz)
   bool b_halo_ok = false; // ghost planes of b are current (fused sweep on rank slabs)
@@ -481,7 +478,6 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipHostMalloc(&hscal_, sizeof(double) * 4, hipHostMallocDefault));
     build_operators();
     build_coarse_inverse();
-    setup_tail();
     setup_peer();
     tuned_ms_.clear();
     for (int l = 0; l < nl; ++l) tune_placement(l);  // levels of >= 2^24 voxels: 0, and 1 at 512^3
@@ -842,10 +838,7 @@ class Solver final : public SolverBase {
     L.x_halo_ok = true;
     L.x_peer_pending = true;
   }
-  void check_device_errors() override {
-    peer_check();
-    tail_check();
-  }
+  void check_device_errors() override { peer_check(); }
   // a peer wait that timed out (a neighbour never delivered) is an error, not silent stale halos
   void peer_check() {
     for (auto& L : lv_) {
@@ -1761,139 +1754,6 @@ class Solver final : public SolverBase {
     HIP_CHECK(hipGetLastError());
   }
 
-  // ------------------------------------------------------------- V-cycle tail
-  // The replicated 3D levels of <= MAD_TAIL_MAX_VOXELS voxels and everything coarser run as ONE vtail_k
-  // launch of NWG workgroups with each level's own planes resident in LDS (mad_kernels.hpp), instead of
-  // ~19 launches per level -- multicolour GS (per-colour levels), dense coarsest inverse, not verbose.
-  // Bit-identical to the launches; MAD_OPT_NO_VCYCLE_TAIL runs the launches (the A/B).  NWG starts at
-  // MAD_TAIL_WGS and doubles until the levels' planes fit the LDS.
-#ifndef MAD_TAIL_MAX_VOXELS
-#define MAD_TAIL_MAX_VOXELS 32768
-#endif
-#ifndef MAD_TAIL_WGS
-#define MAD_TAIL_WGS 16
-#endif
-  static constexpr size_t TAIL_LDS_MAX = 160 * 1024 - 256;
-  struct TailPlan {
-    int nwg = 0;
-    size_t lds = 0;
-    int ppw[TAIL_MAX_LEVELS] = {};
-    uint32_t off[TAIL_MAX_LEVELS] = {};
-  };
-  bool tail_level_ok(int q) const {
-    const Geo& g = lv_[q].g;
-    return c_->dim == 3 && !c_->geom[q].distributed && !lv_[q].brec && g.N <= MAD_TAIL_MAX_VOXELS &&
-           g.sy == g.nx && g.sz == (int64_t)g.nx * g.ny && g.zoff == 0 && g.nz >= 2;
-  }
-  bool tail_plan(int l, TailPlan* p) const {
-    const int nl = c_->nlev;
-    const auto& d = c_->d;
-    if (c_->dim != 3 || d.smoother != MAD_GAUSS_SEIDEL || d.verbose || d.iterations_per_grid < 1) return false;
-    if ((d.options & MAD_OPT_NO_VCYCLE_TAIL) || (l == 0 && c_->bench_trace())) return false;
-    if (nl - l < 2 || nl - l > TAIL_MAX_LEVELS || cblk_.active() || !inv_ || !tail_sync_) return false;
-    if (c_->ncolors != 2 && c_->ncolors != 4) return false;
-    for (int q = l; q < nl - 1; ++q)
-      if (!tail_level_ok(q) || use_fused(q) || !lv_[q].xch) return false;
-    const Geo& gc = lv_[nl - 1].g;
-    if (c_->geom[nl - 1].distributed || gc.sy != gc.nx || gc.zoff != 0 || !lv_[nl - 1].xch) return false;
-    for (int nwg = MAD_TAIL_WGS;; nwg *= 2) {
-      size_t off = 0;
-      for (int q = l; q < nl - 1; ++q) {
-        const Geo& g = lv_[q].g;
-        const int ppw = (g.nz + nwg - 1) / nwg;
-        p->ppw[q - l] = ppw;
-        p->off[q - l] = (uint32_t)off;
-        off += ((size_t)(ppw + 2) + 2 * (size_t)ppw + (size_t)ncoef_ * ppw) * g.sz * sizeof(T);
-        off = (off + 15) & ~(size_t)15;
-      }
-      if (off <= TAIL_LDS_MAX) {
-        p->nwg = nwg;
-        p->lds = off;
-        return true;
-      }
-      if (nwg >= lv_[l].g.nz || nwg >= 64) return false;
-    }
-  }
-  void setup_tail() {
-    const int nl = c_->nlev;
-    int64_t xy = 0;
-    bool any = false;
-    for (int q = 0; q + 1 < nl; ++q) {
-      if (!tail_level_ok(q)) continue;
-      LevelData<T>& L = lv_[q];
-      HIP_CHECK(hipMalloc(&L.xch, sizeof(T) * 2 * L.g.N));
-      xy = std::max<int64_t>(xy, (int64_t)L.g.nz * lv_[q + 1].g.sz);
-      any = true;
-    }
-    if (!any) return;
-    if (!c_->geom[nl - 1].distributed)  // the coarsest level's b and x hand-over
-      HIP_CHECK(hipMalloc(&lv_[nl - 1].xch, sizeof(T) * 2 * lv_[nl - 1].g.N));
-    HIP_CHECK(hipMalloc(&tail_xy_, sizeof(T) * xy));
-    HIP_CHECK(hipMalloc(&tail_sync_, 4 * sizeof(unsigned)));
-    HIP_CHECK(hipMemsetAsync(tail_sync_, 0, 4 * sizeof(unsigned), c_->stream));
-    int wall_khz = 0;
-    if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, c_->device) != hipSuccess ||
-        wall_khz <= 0)
-      wall_khz = 100000;
-    tail_tmo_ = (uint64_t)wall_khz * 1000ull * 2ull;  // 2 s per barrier
-  }
-  bool tail_used_ = false;
-  void tail_check() {
-    if (!tail_used_) return;
-    unsigned err = 0;
-    HIP_CHECK(hipMemcpyAsync(&err, tail_sync_ + 2, sizeof err, hipMemcpyDeviceToHost, c_->stream));
-    HIP_CHECK(hipStreamSynchronize(c_->stream));
-    if (err) throw MadError(MAD_ERR_DEVICE, "V-cycle tail: a workgroup never reached a barrier (timed out)");
-  }
-  void launch_tail(int l, const TailPlan& p) {
-    const int nl = c_->nlev;
-    TailArgs<T> a{};
-    a.nlev = nl - l;
-    a.nu = (int)c_->d.iterations_per_grid;
-    a.ncolors = c_->ncolors;
-    a.inv = inv_;
-    a.xy = tail_xy_;
-    a.sync = tail_sync_;
-    a.tmo = tail_tmo_;
-    for (int q = l; q < nl; ++q) {
-      LevelData<T>& L = lv_[q];
-      TailLevel<T>& t = a.lv[q - l];
-      if (L.x_peer_pending) peer_resolve(q);
-      t.x = L.x;
-      t.b = L.b;
-      t.cf = L.cf;
-      t.xch = L.xch;
-      t.g = L.g;
-      t.rat = L.rat;
-      for (int d = 0; d < 3; ++d) t.cent[d] = L.cent[d];
-      t.ppw = q < nl - 1 ? p.ppw[q - l] : 0;
-      t.lds = q < nl - 1 ? p.off[q - l] : 0;
-      if (q > l) b_changed(q);
-      x_changed(q);
-    }
-    dispatch(3, c_->kind, [&](auto D, auto K) {
-      (void)D;
-      auto kern = vtail_k<T, K.value>;
-      static std::vector<const void*> attr;  // the dynamic-LDS opt-in, once per instance
-      if (std::find(attr.begin(), attr.end(), (const void*)kern) == attr.end()) {
-        HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)TAIL_LDS_MAX));
-        attr.push_back((const void*)kern);
-      }
-      hipLaunchKernelGGL(kern, dim3((unsigned)p.nwg), dim3(256), p.lds, c_->stream, a);
-    });
-    HIP_CHECK(hipGetLastError());
-    tail_used_ = true;
-  }
-  // the tail's launch shape from level l (mad_tail_plan): false when the per-level launches run
-  bool tail_shape(int l, int* nwg, size_t* lds) const override {
-    TailPlan p;
-    if (!tail_plan(l, &p)) return false;
-    *nwg = p.nwg;
-    *lds = p.lds;
-    return true;
-  }
-
   // ------------------------------------------------------------- cycles
   void vcycle_rec(int l) {
     const int nl = c_->nlev;
@@ -1901,13 +1761,6 @@ class Solver final : public SolverBase {
       coarse_solve();
       if (c_->d.verbose) (void)verbose_line(l, -1, "direct solver");
       return;
-    }
-    {
-      TailPlan tp;
-      if (tail_plan(l, &tp)) {  // this level and every coarser one in one launch
-        launch_tail(l, tp);
-        return;
-      }
     }
     const unsigned nu = c_->d.iterations_per_grid;
     const bool bt = l == 0 && c_->bench_trace() && c_->trace_active;  // MAD.hxx:401-409
@@ -2655,9 +2508,6 @@ class Solver final : public SolverBase {
   double* scal_ = nullptr;
   double* hscal_ = nullptr;
   double* inv_ = nullptr;
-  T* tail_xy_ = nullptr;            // vtail_k restriction scratch
-  unsigned* tail_sync_ = nullptr;   // vtail_k barrier / finish counters, sticky error
-  uint64_t tail_tmo_ = 0;
   CoarseBlocks cblk_;  // coarsest levels above DENSE_COARSE_MAX unknowns
   void* scratch_ = nullptr;
   size_t scratch_cap_ = 0;
@@ -2699,12 +2549,7 @@ class Solver final : public SolverBase {
         if (a) (void)hipFree(a);
       if (L.cf_alloc) (void)hipFree(L.cf_alloc);
       if (L.bs_alloc) (void)hipFree(L.bs_alloc);
-      if (L.xch) (void)hipFree(L.xch);
     }
-    if (tail_xy_) (void)hipFree(tail_xy_);
-    if (tail_sync_) (void)hipFree(tail_sync_);
-    tail_xy_ = nullptr;
-    tail_sync_ = nullptr;
     lv_.clear();
     for (auto& a : r64alloc_)
       if (a) (void)hipFree(a), a = nullptr;
@@ -3346,7 +3191,7 @@ int mad_create(const mad_desc* d, mad_ctx** out) {
             MAD_ERR_INVALID, "gs_kernel must be 0, 1, 3 or 4");
     REQUIRE((d->options & ~(MAD_OPT_EAGER_RANK_VCYCLE | MAD_OPT_OVERLAP_RANK_SWEEP | MAD_OPT_PEER_HALO |
                             MAD_OPT_COARSE_NO_CHAIN | MAD_OPT_BENCHMARK_TRACE |
-                            MAD_OPT_NO_PLACEMENT_TUNE | MAD_OPT_NO_RECORD_B | MAD_OPT_NO_VCYCLE_TAIL)) == 0,
+                            MAD_OPT_NO_PLACEMENT_TUNE | MAD_OPT_NO_RECORD_B)) == 0,
             MAD_ERR_INVALID, "unknown option bits");
     REQUIRE(d->min_slab_planes >= 0, MAD_ERR_INVALID, "min_slab_planes must be >= 0");
     REQUIRE(d->min_slab_voxels >= 0, MAD_ERR_INVALID, "min_slab_voxels must be >= 0");
@@ -3580,18 +3425,6 @@ int mad_placement_trials(const mad_ctx* c, uint32_t cap, double* ms, uint32_t* c
   for (size_t q = 0; q < v.size() && q < cap; ++q)
     if (ms) ms[q] = v[q];
   *count = (uint32_t)v.size();
-  return MAD_OK;
-}
-
-int mad_vcycle_tail(const mad_ctx* c, int32_t level, int32_t* workgroups, int64_t* lds_bytes) {
-  if (!c || !workgroups) return MAD_ERR_INVALID;
-  if (!c->solver) return MAD_ERR_STATE;
-  if (level < 0 || level >= c->nlev) return MAD_ERR_INVALID;
-  int nwg = 0;
-  size_t lds = 0;
-  if (!c->solver->tail_shape(level, &nwg, &lds)) nwg = 0, lds = 0;
-  *workgroups = nwg;
-  if (lds_bytes) *lds_bytes = (int64_t)lds;
   return MAD_OK;
 }
 

@@ -315,13 +315,6 @@ class Solver:
         self._check(self._L.mad_placement_trials(self._ctx, k, ms, ctypes.byref(n)))
         return [ms[q] for q in range(k)]
 
-    def vcycle_tail(self, level=1):
-        """(workgroups, LDS bytes) of the one-launch V-cycle tail a V-cycle entering `level` runs
-        (mad_vcycle_tail); (0, 0) when that level runs the per-level launches."""
-        n, b = ctypes.c_int32(), ctypes.c_int64()
-        self._check(self._L.mad_vcycle_tail(self._ctx, level, ctypes.byref(n), ctypes.byref(b)))
-        return n.value, b.value
-
     @property
     def resolved_precision(self):
         """The precision mad_create resolved (PRECISION_AUTO -> FP32 or FP32_REFINE)."""
