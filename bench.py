@@ -395,6 +395,8 @@ def main():
                 s.close()
                 opts = 0
                 s = make(M.SMOOTHER, 0, "sweep-rccl")
+    placement = s.placement_trials()
+
     def barrier():
         s.synchronize()
         if world > 1:
@@ -416,7 +418,8 @@ def main():
     dev_ms, kern_ms, launches = s.bench_smooth(0, a.steps)
     barrier()
     wall = time.perf_counter() - t0
-    per_launch = sorted(s.bench_launch_times())
+    launch_series = list(s.bench_launch_times())  # in launch order (even: read x / write t, odd: the reverse)
+    per_launch = sorted(launch_series)
     if world > 1:
         wall = float(s.allreduce([wall], "max")[0])
     # beside the contract's K steps (24 ms at K = 20): a sustained window of ~2 s of the same
@@ -424,6 +427,9 @@ def main():
     sus_n = max(a.steps, int(2000.0 / max(wall / a.steps * 1e3, 0.05)))
     phase(rank, f"sweeps: sustained window of {sus_n}")
     sus_dev, sus_kern, _ = s.bench_smooth(0, sus_n)
+    sus_series = list(s.bench_launch_times())
+    sus_win = [round(sum(sus_series[q:q + 100]) / len(sus_series[q:q + 100]), 4)
+               for q in range(0, len(sus_series), 100)]
     if world > 1:
         sus_dev = float(s.allreduce([sus_dev], "max")[0])
     nvox = float(S) ** 3
@@ -477,6 +483,7 @@ def main():
             "kernel_ms_mean": round(kern_ms, 5), "launches": launches,
             "kernel_ms_median": round(per_launch[len(per_launch) // 2], 5) if per_launch else None,
             "kernel_ms_min": round(per_launch[0], 5) if per_launch else None,
+            "kernel_ms_series": [round(v, 4) for v in launch_series],
             "algorithmic_bytes_per_launch": BYTES_PER_VOXEL_SMOOTH * units_per_launch}
     if traffic:
         roof["traffic_source"] = traffic.get("source")
@@ -515,8 +522,12 @@ def main():
         "device_ms_per_step": round(dev_ms / a.steps, 4),
         "sustained": {"steps": sus_n, "device_ms_per_step": round(sus_dev / sus_n, 4),
                       "kernel_ms_mean": round(sus_kern, 5),
+                      "kernel_ms_per_100": sus_win,
                       "value": round(nvox * sus_n / (sus_dev * 1e-3) / 1e6, 1)},
         "roofline": roof,
+        # the level-0 sweep ms (forward, reverse direction) of every set of arrays setup tried, the
+        # fastest kept (mad_placement_trials, DESIGN.md "Placement"): which speeds this box offered
+        "placement_trials_ms": [round(v, 4) for v in placement],
     }
     if world == 1 and not a.no_precision_cycles:
         # the cycle mad_run runs at the reference tests' Tolerance 1e-10 (MAD_PRECISION_AUTO ->

@@ -485,22 +485,24 @@ class Solver final : public SolverBase {
   }
 
   // ------------------------------------------------------------- level-0 placement
-  // The level-0 sweep streams ~7 GB per launch at 512^3, and on some boxes its speed depends on where
-  // its arrays landed in physical memory: per allocation, each direction of the ping-pong pair (read x
-  // / write t, then read t / write x) sweeps in ~1.13 or in ~1.24 ms -- the same kernel, the same HBM
-  // bytes, the same L2 hit rate and ~7 K UTCL1 misses per launch in every case, the clocks steady; on
-  // other boxes every allocation runs 1.24 ms (profiles/r06_placement.md).  So setup times both
-  // directions of the level's own sweep on its arrays and on fresh allocations of them (the pair each
-  // time, the records too every second time; contents copied over) and keeps the fastest set, the
-  // others freed: at least PLACEMENT_MIN_TRIES sets, then until both directions of the kept set are within
-  // 2 % of the fastest direction seen once a slower speed has shown up, at most PLACEMENT_TRIES sets.  3D levels of >= 2^24 voxels
-  // (a rank's slab too: 512 x 512 x 64 on 8 ranks) whose sweep is the fused GS sweep -- timed as the
-  // plain whole-slab launch, no exchange, so every rank decides alone -- or, on one rank, the WJ sweep;
-  // with the memory for a second set.  Not on the in-process transport (its ranks share one device).
-  // MAD_OPT_NO_PLACEMENT_TUNE keeps the first allocation.  Every level of >= 2^24 voxels is tuned so
-  // (level 1 of a 512^3 grid too); mad_placement_trials reports level 0's trials.
+  // The level-0 sweep streams ~7 GB per launch at 512^3, and its speed depends on the arrays it runs on:
+  // per allocation, each direction of the ping-pong pair (read x / write t, then read t / write x)
+  // settles at ~1.11-1.13 or at ~1.24 ms -- the same kernel, the same HBM bytes, the same L2 hit rate and
+  // ~7 K UTCL1 misses per launch in every case, the clocks steady (profiles/r06_placement.md) -- and
+  // freshly allocated arrays run slower still for their first ~0.3-1 s of use (profiles/
+  // r06_transient_probe.log).  So setup allocates PLACEMENT_TRIES - 1 more sets of the level's arrays (the
+  // pair each time, the records too every second time; contents copied over), sweeps all of them in turn
+  // for MAD_PLACEMENT_AGE_MS of device time, then times both directions of every set and keeps the
+  // fastest, the others freed.  3D levels of >= 2^24 voxels (a rank's slab too: 512 x 512 x 64 on 8
+  // ranks) whose sweep is the fused GS sweep -- timed as the plain whole-slab launch, no exchange, so
+  // every rank decides alone -- or, on one rank, the WJ sweep; as many sets as the free memory allows.
+  // Not on the in-process transport (its ranks share one device).  MAD_OPT_NO_PLACEMENT_TUNE keeps the
+  // first allocation.  Every level of >= 2^24 voxels is tuned so (level 1 of a 512^3 grid too);
+  // mad_placement_trials reports level 0's trials.
   static constexpr int PLACEMENT_TRIES = 8;
-  static constexpr int PLACEMENT_MIN_TRIES = 4;
+#ifndef MAD_PLACEMENT_AGE_MS
+#define MAD_PLACEMENT_AGE_MS 1500.0
+#endif
   void tune_placement(int l) {
     if (c_->dim != 3 || (c_->d.options & MAD_OPT_NO_PLACEMENT_TUNE)) return;
     if (c_->comm.active() && c_->comm.mode() == Comm::LOCAL) return;
@@ -565,19 +567,14 @@ class Solver final : public SolverBase {
       slowest = std::max({slowest, *fwd, *rev});
     };
     sweeps(16);  // the clocks ramp up over the first ~20 launches after the device idled (r06_clock_summaries)
-    Set best{L.alloc[0], L.alloc[3], L.cf_alloc};
-    double bf = 0.0, br = 0.0;
-    time_dirs(&bf, &br);
+    // the candidate sets, allocated up front: the pair each time, the records too every second time
+    std::vector<Set> sets{Set{L.alloc[0], L.alloc[3], L.cf_alloc}};
     for (int tr = 1; tr < PLACEMENT_TRIES; ++tr) {
-      // the kept set is at the fastest speed seen, a slower one has been seen, and at least
-      // PLACEMENT_MIN_TRIES sets were timed (some kernels have three speeds: the split-b sweep
-      // 1.16 / 1.21 / 1.28 ms on one box, profiles/r06_record_b_ab.log)
-      if (tr >= PLACEMENT_MIN_TRIES && slowest > 1.05 * fastest && std::max(bf, br) <= 1.02 * fastest) break;
       const bool with_cf = (tr % 2) == 0;
       size_t free_b = 0, total_b = 0;
       HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
       if (free_b < 2 * (2 * pbytes + (with_cf ? cbytes : 0)) + ((size_t)1 << 30)) break;
-      Set cand{nullptr, nullptr, with_cf ? nullptr : best.cf};
+      Set cand{nullptr, nullptr, with_cf ? nullptr : sets[0].cf};
       bool ok = contiguous_alloc((void**)&cand.x, pbytes) == hipSuccess &&
                 contiguous_alloc((void**)&cand.t, pbytes) == hipSuccess &&
                 (!with_cf || contiguous_alloc((void**)&cand.cf, cbytes) == hipSuccess);
@@ -588,26 +585,47 @@ class Solver final : public SolverBase {
         if (with_cf && cand.cf) (void)hipFree(cand.cf);
         break;
       }
-      HIP_CHECK(hipMemcpyAsync(cand.x, best.x, pbytes, hipMemcpyDeviceToDevice, c_->stream));
-      HIP_CHECK(hipMemcpyAsync(cand.t, best.t, pbytes, hipMemcpyDeviceToDevice, c_->stream));
-      if (with_cf) HIP_CHECK(hipMemcpyAsync(cand.cf, best.cf, cbytes, hipMemcpyDeviceToDevice, c_->stream));
-      point(cand);
+      HIP_CHECK(hipMemcpyAsync(cand.x, sets[0].x, pbytes, hipMemcpyDeviceToDevice, c_->stream));
+      HIP_CHECK(hipMemcpyAsync(cand.t, sets[0].t, pbytes, hipMemcpyDeviceToDevice, c_->stream));
+      if (with_cf) HIP_CHECK(hipMemcpyAsync(cand.cf, sets[0].cf, cbytes, hipMemcpyDeviceToDevice, c_->stream));
+      sets.push_back(cand);
+    }
+    // age them: freshly allocated arrays sweep slower for the first ~0.3-1 s of their use, then settle at
+    // their own speed (profiles/r06_transient_probe.log), so the sets are swept in turn for
+    // MAD_PLACEMENT_AGE_MS of device time before any is timed
+    double aged_ms = 0.0;
+    while (sets.size() > 1 && aged_ms < MAD_PLACEMENT_AGE_MS) {
+      for (const Set& st : sets) {
+        point(st);
+        sweeps(4);
+        for (float v : launch_ms) aged_ms += v;
+      }
+    }
+    double bf = INFINITY, br = INFINITY;
+    size_t kept = 0;
+    for (size_t i = 0; i < sets.size(); ++i) {
+      point(sets[i]);
       double f = 0.0, r = 0.0;
       time_dirs(&f, &r);
-      Set loser = cand;
-      if (f + r < bf + br) {  // keep the candidate
-        loser = best;
-        best = cand;
+      if (f + r < bf + br) {
+        kept = i;
         bf = f;
         br = r;
-      } else {
-        point(best);
       }
-      HIP_CHECK(hipStreamSynchronize(c_->stream));
-      HIP_CHECK(hipFree(loser.x));
-      HIP_CHECK(hipFree(loser.t));
-      if (loser.cf != best.cf) HIP_CHECK(hipFree(loser.cf));
     }
+    const Set best = sets[kept];
+    point(best);
+    HIP_CHECK(hipStreamSynchronize(c_->stream));
+    for (size_t i = 0; i < sets.size(); ++i) {
+      if (i == kept) continue;
+      HIP_CHECK(hipFree(sets[i].x));
+      HIP_CHECK(hipFree(sets[i].t));
+      // records: a set either owns its own or shares the first set's
+      const bool owns_cf = i == 0 || sets[i].cf != sets[0].cf;
+      if (owns_cf && sets[i].cf != best.cf) HIP_CHECK(hipFree(sets[i].cf));
+    }
+    (void)fastest;
+    (void)slowest;
     x_changed(l);
     L.b_halo_ok = L.brec_ok = false;
   }
