@@ -37,6 +37,9 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--trace", required=True)
     p.add_argument("--ktrace", help="kernel_trace.csv of the same run (per-dispatch durations)")
+    p.add_argument("--tail", type=int, default=0,
+                   help="also average the last N level-0 dispatches (the bench's timed + sustained windows; "
+                        "the earlier ones include setup's placement trials)")
     p.add_argument("--fetch")
     p.add_argument("--write")
     p.add_argument("--kernel", required=True)
@@ -70,13 +73,19 @@ def main():
         d = groups[gmax]
         # coarser levels can launch the same grid (z-chunks): keep the level-0 cluster
         # (durations within 40% of the longest dispatch of that grid)
-        d = [v for v in d if v >= 0.6 * max(d)]
+        ref = sorted(d)[(len(d) * 9) // 10]  # (not the maximum: one stalled dispatch would set it)
+        d = [v for v in d if v >= 0.6 * ref]
         lvl0 = sum(d) / len(d) / 1e3
         res["trace_avg_us_level0"] = lvl0
         res["trace_level0_calls"] = len(d)
         lines += [f"level-0 dispatches (grid {gmax} work-items): {len(d)} calls, average "
                   f"{lvl0:.2f} us, min {min(d)/1e3:.2f} us, max {max(d)/1e3:.2f} us "
                   f"(compare bench.py roofline.kernel_ms_mean)"]
+        if a.tail and len(d) >= a.tail:
+            t = d[-a.tail:]
+            res["trace_avg_us_level0_tail"] = sum(t) / len(t) / 1e3
+            lines += [f"the last {a.tail} of them (the bench's timed + sustained windows): average "
+                      f"{sum(t) / len(t) / 1e3:.2f} us, median {sorted(t)[len(t) // 2] / 1e3:.2f} us"]
     if a.fetch and a.write:
         n = float(a.size) ** 3
         fe = per_kernel(a.fetch, "FETCH_SIZE")
