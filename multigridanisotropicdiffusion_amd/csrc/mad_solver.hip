@@ -530,8 +530,6 @@ class Solver final : public SolverBase {
       L.phys[0] = L.x;
       L.phys[1] = L.t;
     };
-    // mean ms of the two launches in each direction: 0 and 2 read x and write t, 1 and 3 the reverse
-    double fastest = INFINITY, slowest = 0.0;
     // fused GS: the plain whole-slab launch on the level's arrays (rank slabs: no exchange; the ghost
     // planes hold zeros like everything but the records here), swapping the pair like the sweep
     auto sweeps = [&](unsigned n) {
@@ -555,6 +553,7 @@ class Solver final : public SolverBase {
       for (unsigned i = 0; i < n; ++i) HIP_CHECK(hipEventElapsedTime(&launch_ms[i], ev[2 * i], ev[2 * i + 1]));
       for (auto& e : ev) (void)hipEventDestroy(e);
     };
+    // mean ms of the two launches in each direction: 0 and 2 read x and write t, 1 and 3 the reverse
     auto time_dirs = [&](double* fwd, double* rev) {
       sweeps(4);
       *fwd = 0.5 * (launch_ms[0] + launch_ms[2]);
@@ -563,8 +562,6 @@ class Solver final : public SolverBase {
         tuned_ms_.push_back(*fwd);
         tuned_ms_.push_back(*rev);
       }
-      fastest = std::min({fastest, *fwd, *rev});
-      slowest = std::max({slowest, *fwd, *rev});
     };
     sweeps(16);  // the clocks ramp up over the first ~20 launches after the device idled (r06_clock_summaries)
     // the candidate sets, allocated up front: the pair each time, the records too every second time
@@ -624,8 +621,6 @@ class Solver final : public SolverBase {
       const bool owns_cf = i == 0 || sets[i].cf != sets[0].cf;
       if (owns_cf && sets[i].cf != best.cf) HIP_CHECK(hipFree(sets[i].cf));
     }
-    (void)fastest;
-    (void)slowest;
     x_changed(l);
     L.b_halo_ok = L.brec_ok = false;
   }
