@@ -981,9 +981,12 @@ class Solver final : public SolverBase {
   // fp64 too (round 4): 256 workgroups -- at 512^3 one z-chunk per 64 x 16 tile column -- against
   // the 2048 of rounds 1-3: level-0 sweep 2.30-2.38 vs 2.77-2.96 ms, V-cycle 15.7-15.9 vs 18.0-18.6 ms
   // (512 / 1024 workgroups in between; profiles/r04_fp64_blocks_ab.log)
+#ifndef MAD_FUSED_BLOCKS  // A/B knob
+#define MAD_FUSED_BLOCKS 256
+#endif
   static FusedCfg fused_cfg() {
     FusedCfg f;
-    f.blocks = 256;
+    f.blocks = MAD_FUSED_BLOCKS;
     return f;
   }
 
