@@ -442,6 +442,7 @@ def main():
     # VCYCLE: level-0 records without b, dense rhs), as GenerateData runs it; the halo form
     # the sweep measurement settled on
     s = make(M.VCYCLE, opts, "vcycle")
+    vplacement = s.placement_trials()
     vnote = None
     if opts and a.halo == "auto":
         # the V-cycle's distributed levels push too (per-colour levels after their last colour
@@ -528,6 +529,7 @@ def main():
         # the level-0 sweep ms (forward, reverse direction) of every set of arrays setup tried, the
         # fastest kept (mad_placement_trials, DESIGN.md "Placement"): which speeds this box offered
         "placement_trials_ms": [round(v, 4) for v in placement],
+        "vcycle_placement_trials_ms": [round(v, 4) for v in vplacement],  # the V-cycle layout's level-0 sweep
     }
     if world == 1 and not a.no_precision_cycles:
         # the cycle mad_run runs at the reference tests' Tolerance 1e-10 (MAD_PRECISION_AUTO ->
