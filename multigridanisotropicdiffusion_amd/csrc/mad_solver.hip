@@ -491,7 +491,9 @@ class Solver final : public SolverBase {
   // ~7 K UTCL1 misses per launch in every case, the clocks steady (profiles/r06_placement.md) -- and
   // freshly allocated arrays run slower still for their first ~0.3-1 s of use (profiles/
   // r06_transient_probe.log).  So setup allocates PLACEMENT_TRIES - 1 more sets of the level's arrays (the
-  // pair each time, the records too every second time; contents copied over), sweeps all of them in turn
+  // pair each time, the records -- and the V-cycle layout's split b -- too every second time; contents
+  // copied over; 12 sets: 1.10 vs 1.13 ms sweeps, 7.31 vs 7.42 ms V-cycles against 8 on one box,
+  // profiles/r06_tries_ab.log), sweeps all of them in turn
   // for MAD_PLACEMENT_AGE_MS of device time, then times both directions of every set and keeps the
   // fastest, the others freed.  3D levels of >= 2^24 voxels (a rank's slab too: 512 x 512 x 64 on 8
   // ranks) whose sweep is the fused GS sweep -- timed as the plain whole-slab launch, no exchange, so
@@ -499,7 +501,10 @@ class Solver final : public SolverBase {
   // Not on the in-process transport (its ranks share one device).  MAD_OPT_NO_PLACEMENT_TUNE keeps the
   // first allocation.  Every level of >= 2^24 voxels is tuned so (level 1 of a 512^3 grid too);
   // mad_placement_trials reports level 0's trials.
-  static constexpr int PLACEMENT_TRIES = 8;
+#ifndef MAD_PLACEMENT_TRIES
+#define MAD_PLACEMENT_TRIES 12
+#endif
+  static constexpr int PLACEMENT_TRIES = MAD_PLACEMENT_TRIES;
 #ifndef MAD_PLACEMENT_AGE_MS
 #define MAD_PLACEMENT_AGE_MS 1500.0
 #endif
@@ -519,11 +524,14 @@ class Solver final : public SolverBase {
       T* x;
       T* t;
       T* cf;
+      T* bs;  // the V-cycle layout's split b (nullptr where the level has none): moves with the records
     };
     auto point = [&](const Set& a) {  // after an even number of sweeps alloc[0] is x's, alloc[3] t's
       L.alloc[0] = a.x;
       L.alloc[3] = a.t;
       L.cf_alloc = a.cf;
+      L.bs_alloc = a.bs;
+      L.bs = a.bs ? a.bs + margin + L.ghost : nullptr;
       L.x = a.x + margin + L.ghost;
       L.t = a.t + margin + L.ghost;
       L.cf = a.cf + margin * L.g.rs + GHOST * cplane;
@@ -565,26 +573,31 @@ class Solver final : public SolverBase {
     };
     sweeps(16);  // the clocks ramp up over the first ~20 launches after the device idled (r06_clock_summaries)
     // the candidate sets, allocated up front: the pair each time, the records too every second time
-    std::vector<Set> sets{Set{L.alloc[0], L.alloc[3], L.cf_alloc}};
+    std::vector<Set> sets{Set{L.alloc[0], L.alloc[3], L.cf_alloc, L.bs_alloc}};
+    const bool has_bs = L.bs_alloc != nullptr;
     for (int tr = 1; tr < PLACEMENT_TRIES; ++tr) {
       const bool with_cf = (tr % 2) == 0;
+      const bool with_bs = with_cf && has_bs;
       size_t free_b = 0, total_b = 0;
       HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-      if (free_b < 2 * (2 * pbytes + (with_cf ? cbytes : 0)) + ((size_t)1 << 30)) break;
-      Set cand{nullptr, nullptr, with_cf ? nullptr : sets[0].cf};
+      if (free_b < 2 * (2 * pbytes + (with_cf ? cbytes : 0) + (with_bs ? pbytes : 0)) + ((size_t)1 << 30)) break;
+      Set cand{nullptr, nullptr, with_cf ? nullptr : sets[0].cf, with_bs ? nullptr : sets[0].bs};
       bool ok = contiguous_alloc((void**)&cand.x, pbytes) == hipSuccess &&
                 contiguous_alloc((void**)&cand.t, pbytes) == hipSuccess &&
-                (!with_cf || contiguous_alloc((void**)&cand.cf, cbytes) == hipSuccess);
+                (!with_cf || contiguous_alloc((void**)&cand.cf, cbytes) == hipSuccess) &&
+                (!with_bs || contiguous_alloc((void**)&cand.bs, pbytes) == hipSuccess);
       if (!ok) {
         (void)hipGetLastError();
         if (cand.x) (void)hipFree(cand.x);
         if (cand.t) (void)hipFree(cand.t);
         if (with_cf && cand.cf) (void)hipFree(cand.cf);
+        if (with_bs && cand.bs) (void)hipFree(cand.bs);
         break;
       }
       HIP_CHECK(hipMemcpyAsync(cand.x, sets[0].x, pbytes, hipMemcpyDeviceToDevice, c_->stream));
       HIP_CHECK(hipMemcpyAsync(cand.t, sets[0].t, pbytes, hipMemcpyDeviceToDevice, c_->stream));
       if (with_cf) HIP_CHECK(hipMemcpyAsync(cand.cf, sets[0].cf, cbytes, hipMemcpyDeviceToDevice, c_->stream));
+      if (with_bs) HIP_CHECK(hipMemcpyAsync(cand.bs, sets[0].bs, pbytes, hipMemcpyDeviceToDevice, c_->stream));
       sets.push_back(cand);
     }
     // age them: freshly allocated arrays sweep slower for the first ~0.3-1 s of their use, then settle at
@@ -617,9 +630,11 @@ class Solver final : public SolverBase {
       if (i == kept) continue;
       HIP_CHECK(hipFree(sets[i].x));
       HIP_CHECK(hipFree(sets[i].t));
-      // records: a set either owns its own or shares the first set's
+      // records (and split b): a set either owns its own or shares the first set's
       const bool owns_cf = i == 0 || sets[i].cf != sets[0].cf;
       if (owns_cf && sets[i].cf != best.cf) HIP_CHECK(hipFree(sets[i].cf));
+      const bool owns_bs = sets[i].bs && (i == 0 || sets[i].bs != sets[0].bs);
+      if (owns_bs && sets[i].bs != best.bs) HIP_CHECK(hipFree(sets[i].bs));
     }
     x_changed(l);
     L.b_halo_ok = L.brec_ok = false;
